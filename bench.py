@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X codon-LM training step (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Workload = BASELINE config C4: TinyGPT 12L8H d512 (hd 64), T=1024, V=68 codons, GELU MLP,
+SEP-segment causal mask, dropout 0.1, label smoothing 0.05, bf16 compute with fp32
+master weights / AdamW, per-GPU microbatch B=16 (weak scaling), synthetic random codon
+batches already resident in HBM.  One step = fwd + CE + bwd + (RCCL all-reduce) + AdamW.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "genomics-lm_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CONFIGS = {
+    # BASELINE.json configs[3] (the metric's config); others are parity-test shapes
+    "c4": dict(n_layer=12, n_head=8, n_embd=512, block_size=1024, batch=16, swiglu=False, rope=False, kv=None),
+    "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, batch=64, swiglu=False, rope=False, kv=None),
+    "c3": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=64, swiglu=True, rope=True, kv=4),
+}
+PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PEAK_HBM_GBS = 8000.0
+
+
+def flops_per_token(c, V=68):
+    d, L, T = c["n_embd"], c["n_layer"], c["block_size"]
+    hd = d // c["n_head"]
+    kvd = (c["kv"] or c["n_head"]) * hd
+    hid = int(8 * d // 3) if c["swiglu"] else 4 * d
+    mlp = 3 * d * hid if c["swiglu"] else 2 * d * hid
+    n_mm = L * (d * (d + 2 * kvd) + d * d + mlp) + d * V
+    # 6*N_mm + 6*L*d*T (causal-exact attention, no recompute)
+    return 6 * n_mm + 6 * L * d * T
+
+
+def time_kernel(fn, iters=20):
+    """Average device duration of fn() on the current stream, HIP events around the launches."""
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def kernel_rooflines(c, B, dev):
+    """Live per-kernel timings of the step's dominant kernels at the bench shapes."""
+    from codonlm_amd import _lib as L
+    from codonlm_amd import ops
+    d, T, H = c["n_embd"], c["block_size"], c["n_head"]
+    hd = d // H
+    M = B * T
+    out = {}
+    g = torch.Generator(device="cpu").manual_seed(0)
+    x = torch.randn(M, d, generator=g).to(dev, torch.bfloat16)
+    w1 = (torch.randn(4 * d, d, generator=g) * 0.05).to(dev, torch.bfloat16)
+    b1 = torch.zeros(4 * d, device=dev)
+    aux = torch.empty(M, 4 * d, dtype=torch.bfloat16, device=dev)
+    y = torch.empty(M, 4 * d, dtype=torch.bfloat16, device=dev)
+    t = time_kernel(lambda: ops.gemm(x, w1, out=y, bias=b1, epilogue=L.EPI_BIAS | L.EPI_GELU, aux_out=aux))
+    fl = 2.0 * M * 4 * d * d
+    out["gemm_fc1_fwd"] = dict(bound="mfma", achieved=fl / t / 1e12, peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                               ms=t * 1e3, flops=fl)
+    qkv = torch.randn(M, 3 * d, generator=g).to(dev, torch.bfloat16)
+    idx = torch.from_numpy(np.random.default_rng(0).integers(4, 68, size=(B, T))).to(dev)
+    seg = ops.segment_starts(idx, 3)
+    t = time_kernel(lambda: ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=1, drop_p=0.1), iters=10)
+    fl = 4.0 * B * H * hd * T * (T + 1) / 2  # causal-exact QK^T + PV
+    out["attn_fwd"] = dict(bound="mfma", achieved=fl / t / 1e12, peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
+                           ms=t * 1e3, flops=fl)
+    return out
+
+
+def cpu_baseline(c):
+    """fp32 CPU restatement of the same step (oracle.CpuTrainer), bounded sample, rank 0 only."""
+    from oracle import tinygpt_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+    threads = max(1, min(threads, 16))
+    torch.set_num_threads(threads)
+    cfg = O.OracleConfig(vocab_size=68, block_size=c["block_size"], n_layer=c["n_layer"], n_head=c["n_head"],
+                         n_embd=c["n_embd"], n_kv_head=c["kv"], use_swiglu=c["swiglu"], use_rope=c["rope"],
+                         dropout=0.1, label_smoothing=0.05)
+    tr = O.CpuTrainer(cfg, O.synthetic_params(cfg, seed=1), lr=3e-4, wd=0.05)
+    Bc, T = 2, c["block_size"]
+    rng = np.random.default_rng(1337)
+    tok = rng.integers(4, 68, size=(Bc, T + 1))
+    x, y = tok[:, :-1], tok[:, 1:]
+    tr.step(x, y, dropout_seed=1)  # warmup
+    n, t0 = 0, time.perf_counter()
+    while n < 3 or (time.perf_counter() - t0) < 10.0:
+        tr.step(x, y, dropout_seed=2 + n)
+        n += 1
+        if time.perf_counter() - t0 > 30.0:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n * Bc * T / dt, "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"{n} fp32 steps of the same model at B={Bc}, T={T} (reference default per-device batch)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-roofline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from codonlm_amd import TinyGPT
+    from codonlm_amd.optim import FusedAdamW
+    from codonlm_amd.training.ddp import DataParallelStep
+
+    c = dict(CONFIGS[args.config])
+    B = args.batch or c["batch"]
+    T = c["block_size"]
+    torch.manual_seed(1337)
+    model = TinyGPT(68, T, n_layer=c["n_layer"], n_head=c["n_head"], n_embd=c["n_embd"], dropout=0.1,
+                    label_smoothing=0.05, n_kv_head=c["kv"], use_swiglu=c["swiglu"], use_rope=c["rope"],
+                    compute_dtype=args.dtype, device=dev)
+    if world > 1:  # identical replicas
+        dist.broadcast(model.flat_parameters(), 0)
+    model.train()
+    opt = FusedAdamW(model, lr=3e-4, weight_decay=0.05)
+    stepper = DataParallelStep(model, opt)
+
+    rng = np.random.default_rng(1337 + rank)
+    nbuf = 4
+    batches = []
+    for _ in range(nbuf):
+        tok = rng.integers(4, 68, size=(B, T + 1))
+        xb = torch.from_numpy(tok[:, :-1].copy()).to(dev)
+        yb = torch.from_numpy(tok[:, 1:].copy()).to(dev)
+        batches.append((xb, yb))
+
+    def run(i):
+        xb, yb = batches[i % nbuf]
+        return stepper.step(xb, yb, seed=1000 + i)
+
+    for i in range(args.warmup):
+        loss = run(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = run(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(loss.item())
+
+    tokens = world * B * T * args.steps
+    value = tokens / elapsed
+    ftok = flops_per_token(c)
+    result = {
+        "metric": "codon tokens/sec training step, 12L8H d512 seq1024" if args.config == "c4"
+        else f"codon tokens/sec training step ({args.config})",
+        "value": round(value, 1),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (uniform random codons 4..67, resident in HBM; random-init weights)",
+        "config": {"workload": f"TinyGPT {c['n_layer']}L{c['n_head']}H d{c['n_embd']} T{T} V68 train step",
+                   "model": "TinyGPT (genomics-lm src/codonlm)", "global_batch": world * B, "seq_len": T,
+                   "micro_batch_per_gpu": B, "parallelism": f"dp{world}", "dropout": 0.1,
+                   "label_smoothing": 0.05, "sep_mask": True},
+        "final_loss": round(final_loss, 4),
+        "model_flops_per_token": ftok,
+        "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),
+    }
+    if rank == 0 and not args.no_kernel_roofline and args.dtype == "bf16":
+        ks = kernel_rooflines(c, B, dev)
+        dom = max(ks, key=lambda k: ks[k]["ms"])
+        r = ks[dom]
+        result["roofline"] = {"kernel": dom, "bound": r["bound"], "achieved": round(r["achieved"], 2),
+                              "peak": r["peak"], "unit": r["unit"], "frac": round(r["achieved"] / r["peak"], 4),
+                              "traffic": None}
+        result["kernels"] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                             for k, v in ks.items()}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(c)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,137 @@
+"""ctypes binding of libcodonlm_hip.so (include/codonlm_hip.h).
+
+The library is the product path: if it is missing or fails to load this module raises
+immediately -- there is no CPU or PyTorch fallback anywhere in ``codonlm_amd``.
+torch is imported first so the HIP runtime the .so binds to (libamdhip64.so.7) is the
+one PyTorch already loaded (same SONAME => one runtime, shared streams and memory).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
+
+LIB_PATH = Path(__file__).resolve().parent / "libcodonlm_hip.so"
+
+CG_F32, CG_BF16 = 0, 1
+CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
+EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM = 1, 2, 4, 8, 16, 32
+
+# parameter kinds (enum in the header)
+(P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,
+ P_PROJ_B, P_LN2_W, P_LN2_B, P_FC1_W, P_FC1_B, P_FC2_W, P_FC2_B, P_GATE_W, P_UP_W, P_DOWN_W,
+ P_LNF_W, P_LNF_B, P_HEAD_W, P_TERM_W, P_TERM_B, P_OFF1_W, P_OFF1_B, P_OFF2_W, P_OFF2_B) = range(30)
+
+vp = C.c_void_p
+i32, i64, f32, u32, sz = C.c_int, C.c_longlong, C.c_float, C.c_uint32, C.c_size_t
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [("in_dtype", i32), ("c_dtype", i32), ("M", i32), ("N", i32), ("K", i32),
+                ("A", vp), ("lda", i64), ("a_kcontig", i32),
+                ("B", vp), ("ldb", i64), ("b_kcontig", i32),
+                ("C", vp), ("ldc", i64), ("epilogue", i32), ("alpha", f32),
+                ("bias", vp), ("resid", vp), ("ldr", i64),
+                ("aux", vp), ("aux_out", vp), ("ld_aux", i64),
+                ("drop_seed", u32), ("drop_p", f32), ("split_k", i32), ("workspace", vp)]
+
+
+class AdamwSegment(C.Structure):
+    _fields_ = [("begin", i64), ("end", i64), ("lr", f32), ("wd", f32)]
+
+
+class ModelCfg(C.Structure):
+    _fields_ = [("vocab_size", i32), ("block_size", i32), ("n_layer", i32), ("n_head", i32),
+                ("n_kv_head", i32), ("n_embd", i32), ("use_swiglu", i32), ("use_rope", i32),
+                ("sep_id", i32), ("tie_embeddings", i32), ("termination_aux", i32),
+                ("termination_n_classes", i32), ("n_offsets", i32), ("offsets", i32 * 8),
+                ("dropout", f32), ("label_smoothing", f32), ("ln_eps", f32), ("dtype", i32)]
+
+
+class ParamEntry(C.Structure):
+    _fields_ = [("kind", i32), ("layer", i32), ("offset", i64), ("rows", i32), ("cols", i32), ("ld", i64)]
+
+
+class Model(C.Structure):
+    _fields_ = [("cfg", ModelCfg), ("params", vp), ("shadow", vp), ("grads", vp),
+                ("loss_weights", vp), ("rope_cos", vp), ("rope_sin", vp),
+                ("workspace", vp), ("workspace_bytes", sz),
+                ("B", i32), ("T", i32), ("training", i32), ("window", i32), ("seed", u32),
+                ("idx", vp), ("targets", vp), ("logits", vp)]
+
+
+# name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
+SIGNATURES = {
+    "cg_gemm": (i32, [C.POINTER(GemmDesc), vp]),
+    "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
+    "cg_layernorm_bwd_blocks": (i32, [i32]),
+    "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, vp, vp,
+                               i32, i32, i32, f32, vp]),
+    "cg_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, u32, f32, vp]),
+    "cg_embed_bwd_workspace": (sz, [i32, i32, i32, i32]),
+    "cg_embed_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, u32, f32, i32, vp, vp]),
+    "cg_segment_starts": (i32, [vp, vp, i32, i32, i32, vp]),
+    "cg_rope_tab": (i32, [i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, i32, vp]),
+    "cg_attn_fwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp]),
+    "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
+    "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
+                          u32, f32, vp, vp]),
+    "cg_ce_workspace": (sz, [i32]),
+    "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, vp]),
+    "cg_swiglu_fwd": (i32, [i32, vp, i64, i32, vp, i64, i32, i32, vp]),
+    "cg_swiglu_bwd": (i32, [i32, vp, i64, i32, vp, i64, vp, i64, i32, i32, vp]),
+    "cg_colsum_workspace": (sz, [i32, i32]),
+    "cg_colsum": (i32, [i32, vp, i64, i32, i32, vp, i32, vp, vp]),
+    "cg_cast_f32_to_bf16": (i32, [vp, vp, i64, vp]),
+    "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),
+    "cg_adamw": (i32, [vp, vp, vp, vp, vp, C.POINTER(AdamwSegment), i32, f32, f32, f32, i32, f32, vp]),
+    "cg_nonfinite_flag": (i32, [vp, i64, vp, vp]),
+    "cg_model_param_layout": (i32, [C.POINTER(ModelCfg), C.POINTER(ParamEntry), i32, C.POINTER(i64)]),
+    "cg_model_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
+    "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
+    "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),
+    "cg_model_hidden": (vp, [C.POINTER(Model), i32, C.POINTER(i32), C.POINTER(i64)]),
+    "cg_version": (C.c_char_p, []),
+}
+
+
+class LibraryError(RuntimeError):
+    pass
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise LibraryError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C genomics-lm_amd/csrc). codonlm_amd has no CPU fallback.")
+    lib = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int, what: str) -> None:
+    if status == CG_OK:
+        return
+    if status == CG_EINVAL:
+        raise ValueError(f"{what}: invalid argument (CG_EINVAL)")
+    if status == CG_EUNSUPPORTED:
+        raise ValueError(f"{what}: unsupported shape/dtype (CG_EUNSUPPORTED)")
+    raise RuntimeError(f"{what}: kernel launch failed (status {status})")
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_device(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: tensor must live on the MI355X (got {t.device}); "
+                           "codonlm_amd has no CPU path")

@@ -1,0 +1,151 @@
+"""Tensor-level wrappers over the op entry points of libcodonlm_hip.so.
+
+Each wrapper validates shapes, allocates outputs with torch on the tensor's device and
+launches on the current HIP stream.  These are the building blocks the engine uses
+natively; they are exposed for op-level parity tests and for callers that compose
+their own step (e.g. the auxiliary heads).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib as L
+
+_DT = {torch.float32: L.CG_F32, torch.bfloat16: L.CG_BF16}
+
+
+def _dt(t: torch.Tensor) -> int:
+    if t.dtype not in _DT:
+        raise ValueError(f"unsupported dtype {t.dtype}")
+    return _DT[t.dtype]
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=None, out_dtype=None,
+         bias=None, resid=None, epilogue=0, aux=None, aux_out=None, alpha=1.0, drop_seed=0, drop_p=0.0,
+         split_k=1):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); A(m,k)=a[m,k] if a_kcontig else a[k,m]; same for B."""
+    for t in (a, b):
+        L.require_device(t, "gemm")
+    if a.dtype != b.dtype:
+        raise ValueError("a and b must share a dtype")
+    if M is None:
+        M = a.shape[0] if a_kcontig else a.shape[1]
+    if K is None:
+        K = a.shape[1] if a_kcontig else a.shape[0]
+    if N is None:
+        N = b.shape[0] if b_kcontig else b.shape[1]
+    out_dtype = out_dtype or (out.dtype if out is not None else a.dtype)
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=a.device)
+    ws = None
+    if split_k > 1:
+        ws = torch.empty(split_k * M * N, dtype=torch.float32, device=a.device)
+    d = L.GemmDesc()
+    d.in_dtype, d.c_dtype = _dt(a), _dt(out)
+    d.M, d.N, d.K = M, N, K
+    d.A, d.lda, d.a_kcontig = a.data_ptr(), a.stride(0), int(a_kcontig)
+    d.B, d.ldb, d.b_kcontig = b.data_ptr(), b.stride(0), int(b_kcontig)
+    d.C, d.ldc = out.data_ptr(), out.stride(0)
+    d.epilogue = int(epilogue)
+    d.alpha = float(alpha)
+    d.bias = _p(bias)
+    d.resid, d.ldr = _p(resid), (resid.stride(0) if resid is not None else 0)
+    d.aux = _p(aux)
+    d.aux_out = _p(aux_out)
+    aux_t = aux if aux is not None else aux_out
+    d.ld_aux = aux_t.stride(0) if aux_t is not None else 0
+    d.drop_seed, d.drop_p = int(drop_seed) & 0xFFFFFFFF, float(drop_p)
+    d.split_k, d.workspace = int(split_k), _p(ws)
+    L.check(L.lib.cg_gemm(C.byref(d), L.stream_ptr(a.device)), "cg_gemm")
+    return out
+
+
+def layernorm_fwd(x, weight, bias, out_dtype=torch.float32, eps=1e-5):
+    L.require_device(x, "layernorm_fwd")
+    rows, cols = x.shape
+    y = torch.empty(rows, cols, dtype=out_dtype, device=x.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    L.check(L.lib.cg_layernorm_fwd(_dt(y), x.data_ptr(), x.stride(0), weight.data_ptr(), bias.data_ptr(),
+                                   y.data_ptr(), y.stride(0), mean.data_ptr(), rstd.data_ptr(), rows, cols, eps,
+                                   L.stream_ptr(x.device)), "cg_layernorm_fwd")
+    return y, mean, rstd
+
+
+def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5):
+    rows, cols = x.shape
+    g_out = torch.empty(rows, cols, dtype=torch.float32, device=x.device)
+    nblk = L.lib.cg_layernorm_bwd_blocks(rows)
+    part = torch.empty(nblk * 2 * cols, dtype=torch.float32, device=x.device)
+    dgamma = torch.empty(cols, dtype=torch.float32, device=x.device)
+    dbeta = torch.empty_like(dgamma)
+    L.check(L.lib.cg_layernorm_bwd(_dt(dy), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
+                                   rstd.data_ptr(), weight.data_ptr(), _p(g_in), g_out.data_ptr(), L.CG_F32, None,
+                                   0, 0.0, part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), 0, rows, cols, eps,
+                                   L.stream_ptr(x.device)), "cg_layernorm_bwd")
+    return g_out, dgamma, dbeta
+
+
+def segment_starts(idx, sep_id):
+    B, T = idx.shape
+    out = torch.empty(B, T, dtype=torch.int32, device=idx.device)
+    L.check(L.lib.cg_segment_starts(idx.contiguous().data_ptr(), out.data_ptr(), B, T,
+                                    -1 if sep_id is None else int(sep_id), L.stream_ptr(idx.device)),
+            "cg_segment_starts")
+    return out
+
+
+def attn_fwd(qkv, segstart, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0):
+    y = torch.empty(B * T, H * hd, dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty(B * H * T, dtype=torch.float32, device=qkv.device)
+    L.check(L.lib.cg_attn_fwd(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
+                              lse.data_ptr(), B, T, H, KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF,
+                              float(drop_p), L.stream_ptr(qkv.device)), "cg_attn_fwd")
+    return y, lse
+
+
+def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0):
+    dqkv = torch.zeros_like(qkv)
+    ws = torch.empty(int(L.lib.cg_attn_bwd_workspace(B, T, H)) // 4 + 1, dtype=torch.float32, device=qkv.device)
+    L.check(L.lib.cg_attn_bwd(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
+                              dy.data_ptr(), dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), B, T, H,
+                              KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF, float(drop_p), ws.data_ptr(),
+                              L.stream_ptr(qkv.device)), "cg_attn_bwd")
+    return dqkv
+
+
+def cross_entropy(logits, targets, eps=0.0, weight=None, ignore_index=0, grad_dtype=torch.float32, pad_to=None):
+    rows, V = logits.shape
+    ldd = pad_to or V
+    dl = torch.empty(rows, ldd, dtype=grad_dtype, device=logits.device)
+    loss = torch.empty((), dtype=torch.float32, device=logits.device)
+    ws = torch.empty(int(L.lib.cg_ce_workspace(rows)) // 4 + 1, dtype=torch.float32, device=logits.device)
+    L.check(L.lib.cg_cross_entropy(logits.data_ptr(), logits.stride(0), targets.contiguous().data_ptr(), rows, V,
+                                   float(eps), _p(weight), int(ignore_index), 1.0, _dt(dl), dl.data_ptr(), ldd,
+                                   loss.data_ptr(), ws.data_ptr(), L.stream_ptr(logits.device)), "cg_cross_entropy")
+    return loss, dl
+
+
+def adamw_(param, grad, exp_avg, exp_avg_sq, step, segments, shadow=None, beta1=0.9, beta2=0.999, eps=1e-8,
+           grad_scale=1.0):
+    """In-place AdamW over flat fp32 buffers; segments: [(begin, end, lr, wd)]."""
+    n = len(segments)
+    segs = (L.AdamwSegment * n)()
+    for i, (b, e, lr, wd) in enumerate(segments):
+        segs[i].begin, segs[i].end, segs[i].lr, segs[i].wd = int(b), int(e), float(lr), float(wd)
+    L.check(L.lib.cg_adamw(param.data_ptr(), grad.data_ptr(), exp_avg.data_ptr(), exp_avg_sq.data_ptr(),
+                           _p(shadow), segs, n, beta1, beta2, eps, int(step), float(grad_scale),
+                           L.stream_ptr(param.device)), "cg_adamw")
+
+
+def cast_to_bf16(x):
+    out = torch.empty(x.numel(), dtype=torch.bfloat16, device=x.device)
+    L.check(L.lib.cg_cast_f32_to_bf16(x.data_ptr(), out.data_ptr(), x.numel(), L.stream_ptr(x.device)),
+            "cg_cast_f32_to_bf16")
+    return out.view(x.shape)

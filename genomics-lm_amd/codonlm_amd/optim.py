@@ -1,0 +1,77 @@
+"""Fused AdamW over TinyGPT's flat parameter buffer (one cg_adamw launch per step).
+
+Semantics follow torch.optim.AdamW as the codon trainer builds it (loop.py:681-731):
+decoupled weight decay, bias-corrected moments, beta=(0.9, 0.999), eps=1e-8, and the
+reference's two param groups -- the "fast" group (offset_projs / termination_head,
+lr_embedding, wd 0) and the backbone group (everything else incl. embeddings, LN and
+biases, lr / weight_decay; the name match at loop.py:689 never hits tok_emb).
+It subclasses torch.optim.Optimizer so torch's LambdaLR / ReduceLROnPlateau drive the
+per-group ``lr`` exactly as in the reference.  ``grad_scale`` folds the
+accumulation-group average (loop.py:145-150) and the DDP 1/world into the same launch.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+
+def _is_fast(name: str) -> bool:
+    return ("transformer.wte" in name or "shape_proj" in name or "offset_projs" in name
+            or "termination_head" in name)
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, model, lr=3e-4, weight_decay=0.05, lr_embedding=None, betas=(0.9, 0.999), eps=1e-8):
+        self.model = model
+        flat = model.flat_parameters()
+        fast, backbone = [], []
+        for name, p in model.named_parameters():
+            (fast if _is_fast(name) else backbone).append((name, p))
+        groups = []
+        if fast:
+            groups.append({"params": [p for _, p in fast], "lr": lr if lr_embedding is None else lr_embedding,
+                           "weight_decay": 0.0})
+        if backbone:
+            groups.append({"params": [p for _, p in backbone], "lr": lr, "weight_decay": weight_decay})
+        super().__init__(groups, dict(lr=lr, weight_decay=weight_decay, betas=betas, eps=eps))
+        self.betas, self.eps = betas, eps
+        # every group must be one contiguous range of the flat buffer
+        base = flat.data_ptr()
+        total = flat.numel()
+        self._ranges = []
+        spans = []
+        for g in self.param_groups:
+            offs = [((p.data_ptr() - base) // 4) for p in g["params"]]
+            ends = [o + (p.storage_offset() - p.storage_offset()) for o, p in zip(offs, g["params"])]
+            del ends
+            spans.append(offs)
+        fast_begin = min(spans[0]) if fast else total
+        if fast:
+            self._ranges = [(fast_begin, total), (0, fast_begin)]
+        else:
+            self._ranges = [(0, total)]
+        self.exp_avg = torch.zeros_like(flat)
+        self.exp_avg_sq = torch.zeros_like(flat)
+        self.step_count = 0
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.model.zero_grad(set_to_none)
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale: float = 1.0):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        segs = []
+        for g, (b, e) in zip(self.param_groups, self._ranges):
+            if e > b:
+                segs.append((b, e, g["lr"], g["weight_decay"]))
+        eng = self.model.engine
+        shadow = eng.shadow if eng.cfg.dtype == "bf16" else None
+        ops.adamw_(self.model.flat_parameters(), self.model.flat_grads(), self.exp_avg, self.exp_avg_sq,
+                   self.step_count, segs, shadow=shadow, beta1=self.betas[0], beta2=self.betas[1], eps=self.eps,
+                   grad_scale=grad_scale)
+        if shadow is not None:
+            eng._shadow_stale = False
+        return loss

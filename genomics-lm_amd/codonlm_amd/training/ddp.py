@@ -1,0 +1,76 @@
+"""Data-parallel training step: one process per GPU, RCCL gradient all-reduce over xGMI
+overlapped with the native backward.
+
+The reference trains single-process (no torch.distributed anywhere); this
+adds the DP exchange the north star asks for.  Gradients live in ONE flat buffer whose
+layout puts each transformer block in its own contiguous range, so each backward phase
+(head/ln_f, block L-1 ... block 0, embeddings) completes exactly one bucket.  Right after
+the engine has *enqueued* a phase's kernels we issue ``all_reduce(bucket, async_op=True)``
+on the RCCL process group: RCCL's stream waits on the compute stream at that point and
+then runs concurrently with the next phase's kernels.  The 1/world average is folded
+into the AdamW launch (``grad_scale``), as is the accumulation-group average
+(loop.py:145-150).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from .. import _lib as L
+
+
+def bucket_ranges(model):
+    """{phase_name: (begin, end)} flat-buffer ranges completed by each backward phase."""
+    lay = model._layout
+    total = model._flat.numel()
+    layer_start = {}
+    lnf = None
+    for kind, layer, off, rows, cols, ld in lay:
+        if kind == L.P_LN1_W:
+            layer_start[layer] = off
+        if kind == L.P_LNF_W:
+            lnf = off
+    L_ = model.n_layer
+    ranges = {"head": (lnf, total)}
+    for l in range(L_):
+        end = layer_start[l + 1] if l + 1 < L_ else lnf
+        ranges[l] = (layer_start[l], end)
+    ranges["embed"] = (0, layer_start[0] if L_ > 0 else lnf)
+    return ranges
+
+
+class DataParallelStep:
+    """fwd + CE + bwd (+ bucketed all-reduce) + AdamW for one microbatch group."""
+
+    def __init__(self, model, optimizer, group=None):
+        self.model = model
+        self.opt = optimizer
+        self.group = group
+        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        self.ranges = bucket_ranges(model)
+
+    def _hook(self, handles):
+        grads = self.model.flat_grads()
+
+        def hook(name):
+            if self.world <= 1:
+                return
+            b, e = self.ranges[name]
+            if e > b:
+                handles.append(dist.all_reduce(grads[b:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        return hook
+
+    def microbatch(self, idx, targets, *, seed: int, accumulate: bool, sync: bool):
+        """Forward + backward of one microbatch; all-reduce only when ``sync`` (last of a group)."""
+        eng = self.model.engine
+        _, loss = eng.forward(idx, targets, training=True, seed=seed)
+        handles = []
+        eng.backward(accumulate=accumulate, bucket_hook=self._hook(handles) if sync else None)
+        return loss, handles
+
+    def step(self, idx, targets, *, seed: int, n_micro: int = 1):
+        loss, handles = self.microbatch(idx, targets, seed=seed, accumulate=False, sync=True)
+        for h in handles:
+            h.wait()
+        self.opt.step(grad_scale=1.0 / (self.world * n_micro))
+        return loss

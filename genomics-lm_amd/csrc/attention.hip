@@ -1,0 +1,338 @@
+// Causal + SEP-segment (+local window) attention with GQA and attention-prob dropout,
+// flash-style (online softmax, no T x T matrix) -- replaces the SDPA / manual path of
+// model_tiny_gpt.py:102-131 with the mask of build_attention_mask (:273-295).
+//
+// Mask for query q, key j (same batch row):  j <= q  &&  j >= segstart[q]
+//                                             && (window <= 0 || q - j < window)
+// (segstart[q] = last SEP position <= q; equal cumsum(idx==SEP) <=> no SEP in (j, q].)
+// Dropout (training): P_ij * keep(seed, (b*H+h)*T+q, j) / (1-p) feeds P.V only; the
+// softmax normaliser uses the undropped P, exactly like att=softmax; att=dropout(att).
+//
+// Two implementations share this contract:
+//   * attn_*_vec   : one query (or key) row per lane, fp32 VALU math.  Any T, hd <= 64,
+//                    fp32 or bf16 storage.  Used for the fp32 parity mode and as the
+//                    bf16 fallback for head dims the MFMA kernel does not cover.
+//   * attn_*_mfma  : bf16 MFMA 32x32x16 kernels (hd in {32, 48, 64}) -- attention_mfma.h
+#include "common.h"
+
+constexpr int AV_HD = 64;   // max head dim of the vector kernels
+constexpr int AV_TQ = 64;   // queries (or keys) per block
+
+__device__ __forceinline__ bool attn_visible(int q, int j, int lo) { return j <= q && j >= lo; }
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_fwd_vec(const T* __restrict__ qkv, long long ld,
+                                                   const int32_t* __restrict__ segstart, T* __restrict__ y,
+                                                   long long ldy, float* __restrict__ lse, int Tn, int H, int KV,
+                                                   int hd, int window, uint32_t seed, uint32_t thr, float dscale,
+                                                   float scale) {
+  __shared__ float Ks[AV_TQ][AV_HD + 1];
+  __shared__ float Vs[AV_TQ][AV_HD + 1];
+  const int lane = threadIdx.x;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H, kvh = h / (H / KV);
+  const int q = blockIdx.x * AV_TQ + lane;
+  const bool qok = q < Tn;
+  const long long qrow = (long long)b * Tn + (qok ? q : 0);
+  float qv[AV_HD], o[AV_HD];
+#pragma unroll
+  for (int d = 0; d < AV_HD; ++d) {
+    qv[d] = (qok && d < hd) ? ld_act<T>(qkv + qrow * ld + (long long)h * hd + d) : 0.f;
+    o[d] = 0.f;
+  }
+  int lo = (qok && segstart) ? segstart[qrow] : 0;
+  if (window > 0) lo = max(lo, q - window + 1);
+  int lo_min = qok ? lo : 0x7fffffff;
+#pragma unroll
+  for (int o2 = 32; o2 > 0; o2 >>= 1) lo_min = min(lo_min, __shfl_xor(lo_min, o2, 64));
+  const int qmax = min(Tn - 1, (int)blockIdx.x * AV_TQ + AV_TQ - 1);
+  const long long koff = (long long)H * hd + (long long)kvh * hd;
+  const long long voff = (long long)(H + KV) * hd + (long long)kvh * hd;
+  const uint32_t drow = (uint32_t)(((long long)b * H + h) * Tn + q);
+  float m = -INFINITY, l = 0.f;
+  for (int k0 = (lo_min / AV_TQ) * AV_TQ; k0 <= qmax; k0 += AV_TQ) {
+    __syncthreads();
+    for (int e = lane; e < AV_TQ * AV_HD; e += 64) {
+      const int j = e / AV_HD, d = e % AV_HD;
+      const int key = k0 + j;
+      const bool ok = key < Tn && d < hd;
+      const long long kr = ((long long)b * Tn + key) * ld;
+      Ks[j][d] = ok ? ld_act<T>(qkv + kr + koff + d) : 0.f;
+      Vs[j][d] = ok ? ld_act<T>(qkv + kr + voff + d) : 0.f;
+    }
+    __syncthreads();
+    float s[AV_TQ];
+    float mt = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < AV_TQ; ++j) {
+      const int key = k0 + j;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < AV_HD; ++d) acc += qv[d] * Ks[j][d];
+      const bool vis = qok && key < Tn && attn_visible(q, key, lo);
+      s[j] = vis ? acc * scale : -INFINITY;
+      mt = fmaxf(mt, s[j]);
+    }
+    const float mn = fmaxf(m, mt);
+    if (mn == -INFINITY) continue;
+    const float alpha = __expf(m - mn);
+    l *= alpha;
+#pragma unroll
+    for (int d = 0; d < AV_HD; ++d) o[d] *= alpha;
+#pragma unroll
+    for (int j = 0; j < AV_TQ; ++j) {
+      float p = __expf(s[j] - mn);
+      l += p;
+      if (thr) p = cg_keep(seed, drow, (uint32_t)(k0 + j), thr) ? p * dscale : 0.f;
+#pragma unroll
+      for (int d = 0; d < AV_HD; ++d) o[d] += p * Vs[j][d];
+    }
+    m = mn;
+  }
+  if (qok) {
+    const float il = 1.0f / l;
+    for (int d = 0; d < hd; ++d) st_act<T>(y + qrow * ldy + (long long)h * hd + d, o[d] * il);
+    lse[((long long)b * H + h) * Tn + q] = m + __logf(l);
+  }
+}
+
+// delta[bh,q] = sum_d dy * y   (rowsum(dO o O), valid with dropout)
+template <typename T>
+__global__ void attn_delta_kernel(const T* __restrict__ y, long long ldy, const T* __restrict__ dy, long long lddy,
+                                  float* __restrict__ delta, int B, int Tn, int H, int hd) {
+  const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (e >= (long long)B * H * Tn) return;
+  const int q = (int)(e % Tn);
+  const long long bh = e / Tn;
+  const int b = (int)(bh / H), h = (int)(bh % H);
+  const long long r = (long long)b * Tn + q;
+  float s = 0.f;
+  for (int d = 0; d < hd; ++d)
+    s += ld_act<T>(dy + r * lddy + (long long)h * hd + d) * ld_act<T>(y + r * ldy + (long long)h * hd + d);
+  delta[e] = s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_dq_vec(const T* __restrict__ qkv, long long ld,
+                                                      const int32_t* __restrict__ segstart, const T* __restrict__ dy,
+                                                      long long lddy, const float* __restrict__ lse,
+                                                      const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                      long long lddq, int Tn, int H, int KV, int hd, int window,
+                                                      uint32_t seed, uint32_t thr, float dscale, float scale) {
+  __shared__ float Ks[AV_TQ][AV_HD + 1];
+  __shared__ float Vs[AV_TQ][AV_HD + 1];
+  const int lane = threadIdx.x;
+  const int bh = blockIdx.y, b = bh / H, h = bh % H, kvh = h / (H / KV);
+  const int q = blockIdx.x * AV_TQ + lane;
+  const bool qok = q < Tn;
+  const long long qrow = (long long)b * Tn + (qok ? q : 0);
+  float qv[AV_HD], dov[AV_HD], dq[AV_HD];
+#pragma unroll
+  for (int d = 0; d < AV_HD; ++d) {
+    const bool ok = qok && d < hd;
+    qv[d] = ok ? ld_act<T>(qkv + qrow * ld + (long long)h * hd + d) : 0.f;
+    dov[d] = ok ? ld_act<T>(dy + qrow * lddy + (long long)h * hd + d) : 0.f;
+    dq[d] = 0.f;
+  }
+  int lo = (qok && segstart) ? segstart[qrow] : 0;
+  if (window > 0) lo = max(lo, q - window + 1);
+  int lo_min = qok ? lo : 0x7fffffff;
+#pragma unroll
+  for (int o2 = 32; o2 > 0; o2 >>= 1) lo_min = min(lo_min, __shfl_xor(lo_min, o2, 64));
+  const long long bhq = ((long long)b * H + h) * Tn + (qok ? q : 0);
+  const float L = qok ? lse[bhq] : 0.f;
+  const float dl = qok ? delta[bhq] : 0.f;
+  const int qmax = min(Tn - 1, (int)blockIdx.x * AV_TQ + AV_TQ - 1);
+  const long long koff = (long long)H * hd + (long long)kvh * hd;
+  const long long voff = (long long)(H + KV) * hd + (long long)kvh * hd;
+  const uint32_t drow = (uint32_t)bhq;
+  for (int k0 = (lo_min / AV_TQ) * AV_TQ; k0 <= qmax; k0 += AV_TQ) {
+    __syncthreads();
+    for (int e = lane; e < AV_TQ * AV_HD; e += 64) {
+      const int j = e / AV_HD, d = e % AV_HD;
+      const int key = k0 + j;
+      const bool ok = key < Tn && d < hd;
+      const long long kr = ((long long)b * Tn + key) * ld;
+      Ks[j][d] = ok ? ld_act<T>(qkv + kr + koff + d) : 0.f;
+      Vs[j][d] = ok ? ld_act<T>(qkv + kr + voff + d) : 0.f;
+    }
+    __syncthreads();
+    for (int j = 0; j < AV_TQ; ++j) {
+      const int key = k0 + j;
+      if (!(qok && key < Tn && attn_visible(q, key, lo))) continue;
+      float sacc = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < AV_HD; ++d) { sacc += qv[d] * Ks[j][d]; dp += dov[d] * Vs[j][d]; }
+      const float p = __expf(sacc * scale - L);
+      if (thr) dp = cg_keep(seed, drow, (uint32_t)key, thr) ? dp * dscale : 0.f;
+      const float ds = p * (dp - dl);
+#pragma unroll
+      for (int d = 0; d < AV_HD; ++d) dq[d] += ds * Ks[j][d];
+    }
+  }
+  if (qok)
+    for (int d = 0; d < hd; ++d) st_act<T>(dqkv + qrow * lddq + (long long)h * hd + d, dq[d] * scale);
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void attn_bwd_dkdv_vec(const T* __restrict__ qkv, long long ld,
+                                                        const int32_t* __restrict__ segstart, const T* __restrict__ dy,
+                                                        long long lddy, const float* __restrict__ lse,
+                                                        const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                        long long lddq, int Tn, int H, int KV, int hd, int window,
+                                                        uint32_t seed, uint32_t thr, float dscale, float scale) {
+  __shared__ float Ks[AV_TQ][AV_HD + 1];
+  __shared__ float Vs[AV_TQ][AV_HD + 1];
+  __shared__ float Qs[AV_TQ][AV_HD];
+  __shared__ float Ds[AV_TQ][AV_HD];
+  __shared__ float Ls[AV_TQ], Dl[AV_TQ];
+  __shared__ int Lo[AV_TQ];
+  const int lane = threadIdx.x;
+  const int bk = blockIdx.y, b = bk / KV, kvh = bk % KV;
+  const int rep = H / KV;
+  const int k0 = blockIdx.x * AV_TQ;
+  const int key = k0 + lane;
+  const bool kok = key < Tn;
+  const long long koff = (long long)H * hd + (long long)kvh * hd;
+  const long long voff = (long long)(H + KV) * hd + (long long)kvh * hd;
+  for (int e = lane; e < AV_TQ * AV_HD; e += 64) {
+    const int j = e / AV_HD, d = e % AV_HD;
+    const bool ok = (k0 + j) < Tn && d < hd;
+    const long long kr = ((long long)b * Tn + k0 + j) * ld;
+    Ks[j][d] = ok ? ld_act<T>(qkv + kr + koff + d) : 0.f;
+    Vs[j][d] = ok ? ld_act<T>(qkv + kr + voff + d) : 0.f;
+  }
+  float dk[AV_HD], dv[AV_HD];
+#pragma unroll
+  for (int d = 0; d < AV_HD; ++d) { dk[d] = 0.f; dv[d] = 0.f; }
+  int qend = Tn;
+  if (window > 0) qend = min(Tn, k0 + AV_TQ - 1 + window);
+  for (int hh = 0; hh < rep; ++hh) {
+    const int h = kvh * rep + hh;
+    const long long bh = (long long)b * H + h;
+    for (int q0 = k0; q0 < qend; q0 += AV_TQ) {
+      __syncthreads();
+      for (int e = lane; e < AV_TQ * AV_HD; e += 64) {
+        const int i = e / AV_HD, d = e % AV_HD;
+        const bool ok = (q0 + i) < Tn && d < hd;
+        const long long r = (long long)b * Tn + q0 + i;
+        Qs[i][d] = ok ? ld_act<T>(qkv + r * ld + (long long)h * hd + d) : 0.f;
+        Ds[i][d] = ok ? ld_act<T>(dy + r * lddy + (long long)h * hd + d) : 0.f;
+      }
+      {
+        const int qi = q0 + lane;
+        const bool ok = qi < Tn;
+        Ls[lane] = ok ? lse[bh * Tn + qi] : 0.f;
+        Dl[lane] = ok ? delta[bh * Tn + qi] : 0.f;
+        int lo = (ok && segstart) ? segstart[(long long)b * Tn + qi] : 0;
+        if (window > 0) lo = max(lo, qi - window + 1);
+        Lo[lane] = ok ? lo : 0x7fffffff;
+      }
+      __syncthreads();
+      if (!kok) continue;
+      for (int i = 0; i < AV_TQ; ++i) {
+        const int qi = q0 + i;
+        if (qi >= Tn || !attn_visible(qi, key, Lo[i])) continue;
+        float sacc = 0.f, dp = 0.f;
+#pragma unroll
+        for (int d = 0; d < AV_HD; ++d) { sacc += Qs[i][d] * Ks[lane][d]; dp += Ds[i][d] * Vs[lane][d]; }
+        const float p = __expf(sacc * scale - Ls[i]);
+        float pd = p;
+        if (thr) {
+          const bool kp = cg_keep(seed, (uint32_t)(bh * Tn + qi), (uint32_t)key, thr);
+          pd = kp ? p * dscale : 0.f;
+          dp = kp ? dp * dscale : 0.f;
+        }
+        const float ds = p * (dp - Dl[i]);
+#pragma unroll
+        for (int d = 0; d < AV_HD; ++d) {
+          dv[d] += pd * Ds[i][d];
+          dk[d] += ds * Qs[i][d];
+        }
+      }
+    }
+  }
+  if (kok) {
+    const long long r = (long long)b * Tn + key;
+    for (int d = 0; d < hd; ++d) {
+      st_act<T>(dqkv + r * lddq + koff + d, dk[d] * scale);
+      st_act<T>(dqkv + r * lddq + voff + d, dv[d]);
+    }
+  }
+}
+
+#include "attention_mfma.h"
+
+// ---------------------------------------------------------------------------
+// host entry points
+// ---------------------------------------------------------------------------
+extern "C" int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, void* y,
+                           long long ldy, float* lse, int B, int T, int H, int KV, int hd, int window,
+                           uint32_t drop_seed, float drop_p, void* stream) {
+  if (KV <= 0 || H % KV) return CG_EINVAL;
+  if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
+  if (B == 0 || T == 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
+  const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const float scale = 1.0f / sqrtf((float)hd);
+  if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, ldy)) {
+    return attn_fwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (bf16_t*)y, ldy, lse, B, T, H, KV, hd, window,
+                                drop_seed, thr, dscale, scale, s);
+  }
+  dim3 g(cg_cdiv(T, AV_TQ), B * H);
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(attn_fwd_vec<bf16_t>, g, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart, (bf16_t*)y,
+                       ldy, lse, T, H, KV, hd, window, drop_seed, thr, dscale, scale);
+  else
+    hipLaunchKernelGGL(attn_fwd_vec<float>, g, dim3(64), 0, s, (const float*)qkv, ldqkv, segstart, (float*)y, ldy,
+                       lse, T, H, KV, hd, window, drop_seed, thr, dscale, scale);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return (size_t)B * H * T * sizeof(float); }
+
+extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const void* y,
+                           long long ldy, const void* dy, long long lddy, const float* lse, void* dqkv,
+                           long long lddqkv, int B, int T, int H, int KV, int hd, int window, uint32_t drop_seed,
+                           float drop_p, void* ws, void* stream) {
+  if (KV <= 0 || H % KV) return CG_EINVAL;
+  if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
+  if (B == 0 || T == 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
+  const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  const float scale = 1.0f / sqrtf((float)hd);
+  float* delta = (float*)ws;
+  const long long nbt = (long long)B * H * T;
+  if (dtype == CG_BF16) {
+    hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const bf16_t*)y, ldy,
+                       (const bf16_t*)dy, lddy, delta, B, T, H, hd);
+  } else {
+    hipLaunchKernelGGL(attn_delta_kernel<float>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const float*)y, ldy,
+                       (const float*)dy, lddy, delta, B, T, H, hd);
+  }
+  CG_LAUNCH_CHECK();
+  if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, lddy) && (lddqkv & 7) == 0) {
+    return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)dy, lddy, lse, delta,
+                                (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr, dscale, scale, s);
+  }
+  dim3 gq(cg_cdiv(T, AV_TQ), B * H), gk(cg_cdiv(T, AV_TQ), B * KV);
+  if (dtype == CG_BF16) {
+    hipLaunchKernelGGL(attn_bwd_dq_vec<bf16_t>, gq, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart,
+                       (const bf16_t*)dy, lddy, lse, delta, (bf16_t*)dqkv, lddqkv, T, H, KV, hd, window, drop_seed,
+                       thr, dscale, scale);
+    hipLaunchKernelGGL(attn_bwd_dkdv_vec<bf16_t>, gk, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart,
+                       (const bf16_t*)dy, lddy, lse, delta, (bf16_t*)dqkv, lddqkv, T, H, KV, hd, window, drop_seed,
+                       thr, dscale, scale);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dq_vec<float>, gq, dim3(64), 0, s, (const float*)qkv, ldqkv, segstart,
+                       (const float*)dy, lddy, lse, delta, (float*)dqkv, lddqkv, T, H, KV, hd, window, drop_seed,
+                       thr, dscale, scale);
+    hipLaunchKernelGGL(attn_bwd_dkdv_vec<float>, gk, dim3(64), 0, s, (const float*)qkv, ldqkv, segstart,
+                       (const float*)dy, lddy, lse, delta, (float*)dqkv, lddqkv, T, H, KV, hd, window, drop_seed,
+                       thr, dscale, scale);
+  }
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}

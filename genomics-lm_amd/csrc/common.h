@@ -1,0 +1,102 @@
+// Shared device helpers for the codon-LM MI355X (gfx950) kernels.
+// Wave = 64 lanes everywhere; all reductions are written for 64-wide waves.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/codonlm_hip.h"
+
+#define CG_WAVE 64
+
+typedef uint16_t bf16_t;  // raw bf16 storage
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef __bf16 v8bf __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+
+// ---------------------------------------------------------------------------
+// bf16 <-> f32 (round-to-nearest-even, NaN preserved)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(bf16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+
+// Typed load/store of one activation element (T = float or bf16_t).
+template <typename T> __device__ __forceinline__ float ld_act(const T* p);
+template <> __device__ __forceinline__ float ld_act<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld_act<bf16_t>(const bf16_t* p) { return bf2f(*p); }
+template <typename T> __device__ __forceinline__ void st_act(T* p, float v);
+template <> __device__ __forceinline__ void st_act<float>(float* p, float v) { *p = v; }
+template <> __device__ __forceinline__ void st_act<bf16_t>(bf16_t* p, float v) { *p = f2bf(v); }
+
+// ---------------------------------------------------------------------------
+// wave / block reductions (64 lanes)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based dropout hash.  keep(seed,row,col) is a pure function so the
+// backward pass regenerates the forward mask.  Restated bit-for-bit in
+// oracle/tinygpt_oracle.py dropout_keep (the parity tests compare them).
+// One 32-bit hash covers the column pair (2c, 2c+1): low half -> even column.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t cg_fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t cg_hash_pair(uint32_t seed, uint32_t row, uint32_t colpair) {
+  uint32_t h = (row * 0x9E3779B1u) ^ (colpair * 0x85EBCA77u) ^ seed;
+  return cg_fmix32(h);
+}
+__device__ __forceinline__ bool cg_keep(uint32_t seed, uint32_t row, uint32_t col, uint32_t thr) {
+  uint32_t h = cg_hash_pair(seed, row, col >> 1);
+  uint32_t bits = (col & 1u) ? (h >> 16) : (h & 0xFFFFu);
+  return bits >= thr;
+}
+__host__ __device__ inline uint32_t cg_drop_threshold(float p) {
+  float t = p * 65536.0f + 0.5f;
+  uint32_t u = (uint32_t)t;
+  return u > 65536u ? 65536u : u;
+}
+__host__ __device__ inline uint32_t cg_site_seed(uint32_t seed, int layer, int site) {
+  uint32_t x = seed * 0x01000193u + (uint32_t)layer * 0x9E37u + (uint32_t)site * 0x7F4A7C15u + 0x3C6EF372u;
+  x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+  return x;
+}
+enum { CG_SITE_EMB = 0, CG_SITE_ATTN = 1, CG_SITE_MLP = 2 };
+
+// GELU (erf form, nn.GELU default) and its derivative
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float dgelu_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+
+// host-side launch check
+#define CG_LAUNCH_CHECK()                                   \
+  do {                                                      \
+    hipError_t _e = hipGetLastError();                      \
+    if (_e != hipSuccess) return CG_ELAUNCH;                \
+  } while (0)
+
+static inline int cg_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

@@ -1,0 +1,515 @@
+// Whole-model engine: the TinyGPT step (model_tiny_gpt.py:297-352 forward, its autograd
+// for loss.backward() at loop.py:1233) sequenced natively as stream-ordered kernel
+// launches.  The flat parameter layout (one fp32 buffer, grads in the same layout, an
+// optional bf16 shadow for the MFMA GEMMs) is owned here; Python builds reference-named
+// nn.Parameter views over it (state_dict compatible with the reference).
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <algorithm>
+#include <vector>
+#include "../../include/codonlm_hip.h"
+
+extern "C" int cg_rope_tab(int dtype, void* qkv, long long ldqkv, int B, int T, int H, int KV, int hd,
+                           const float* cos_tab, const float* sin_tab, int inverse, void* stream);
+
+namespace {
+
+constexpr long long ALIGN = 64;  // elements
+inline long long rup(long long a, long long b) { return (a + b - 1) / b * b; }
+inline uint32_t site_seed(uint32_t seed, int layer, int site) {
+  uint32_t x = seed * 0x01000193u + (uint32_t)layer * 0x9E37u + (uint32_t)site * 0x7F4A7C15u + 0x3C6EF372u;
+  x ^= x >> 16; x *= 0x85EBCA6Bu; x ^= x >> 13; x *= 0xC2B2AE35u; x ^= x >> 16;
+  return x;
+}
+enum { SITE_EMB = 0, SITE_ATTN = 1, SITE_MLP = 2 };
+
+struct Dims {
+  int V, Vp, Tmax, L, H, KV, d, hd, kvd, Nqkv, hid, Hp, swiglu, rope;
+};
+
+bool dims_of(const cg_model_cfg* c, Dims& D) {
+  if (!c || c->n_embd <= 0 || c->n_head <= 0 || c->n_embd % c->n_head) return false;
+  D.V = c->vocab_size;
+  D.Vp = (int)rup(c->vocab_size, 16);
+  D.Tmax = c->block_size;
+  D.L = c->n_layer;
+  D.H = c->n_head;
+  D.KV = (c->n_kv_head > 0 && c->n_kv_head <= c->n_head) ? c->n_kv_head : c->n_head;
+  D.d = c->n_embd;
+  D.hd = c->n_embd / c->n_head;
+  D.kvd = D.KV * D.hd;
+  D.Nqkv = D.d + 2 * D.kvd;
+  D.swiglu = c->use_swiglu != 0;
+  D.rope = c->use_rope != 0;
+  D.hid = D.swiglu ? (int)(8 * (long long)c->n_embd / 3) : 4 * c->n_embd;
+  D.Hp = D.swiglu ? (int)rup(D.hid, 64) : D.hid;
+  return true;
+}
+
+struct Layout {
+  std::vector<cg_param_entry> e;
+  long long total = 0;
+  // per-layer offsets
+  struct Lay {
+    long long ln1w, ln1b, wqkv, bqkv, wp, bp, ln2w, ln2b, w1, b1, w2, b2, wgu, wd;
+  };
+  std::vector<Lay> lay;
+  long long tok, pos = -1, lnfw, lnfb, head = -1, termw = -1, termb = -1;
+  std::vector<long long> off1w, off1b, off2w, off2b;
+};
+
+void build_layout(const cg_model_cfg* c, const Dims& D, Layout& Lo) {
+  long long cur = 0;
+  auto add = [&](int kind, int layer, int rows, int cols, long long ld, long long alloc_elems, bool align) {
+    if (align) cur = rup(cur, ALIGN);
+    cg_param_entry en{kind, layer, cur, rows, cols, ld};
+    Lo.e.push_back(en);
+    long long off = cur;
+    cur += alloc_elems;
+    return off;
+  };
+  const int d = D.d;
+  Lo.tok = add(CG_P_TOK_EMB, -1, D.V, d, d, (long long)D.Vp * d, true);
+  if (!D.rope) Lo.pos = add(CG_P_POS_EMB, -1, D.Tmax, d, d, (long long)D.Tmax * d, true);
+  Lo.lay.resize(D.L);
+  for (int l = 0; l < D.L; ++l) {
+    auto& y = Lo.lay[l];
+    y.ln1w = add(CG_P_LN1_W, l, d, 0, d, d, true);
+    y.ln1b = add(CG_P_LN1_B, l, d, 0, d, d, false);
+    y.wqkv = add(CG_P_Q_W, l, d, d, d, (long long)d * d, true);
+    add(CG_P_K_W, l, D.kvd, d, d, (long long)D.kvd * d, false);
+    add(CG_P_V_W, l, D.kvd, d, d, (long long)D.kvd * d, false);
+    y.bqkv = add(CG_P_Q_B, l, d, 0, d, d, true);
+    add(CG_P_K_B, l, D.kvd, 0, D.kvd, D.kvd, false);
+    add(CG_P_V_B, l, D.kvd, 0, D.kvd, D.kvd, false);
+    y.wp = add(CG_P_PROJ_W, l, d, d, d, (long long)d * d, true);
+    y.bp = add(CG_P_PROJ_B, l, d, 0, d, d, true);
+    y.ln2w = add(CG_P_LN2_W, l, d, 0, d, d, true);
+    y.ln2b = add(CG_P_LN2_B, l, d, 0, d, d, false);
+    if (!D.swiglu) {
+      y.w1 = add(CG_P_FC1_W, l, D.hid, d, d, (long long)D.hid * d, true);
+      y.b1 = add(CG_P_FC1_B, l, D.hid, 0, D.hid, D.hid, true);
+      y.w2 = add(CG_P_FC2_W, l, d, D.hid, D.hid, (long long)d * D.hid, true);
+      y.b2 = add(CG_P_FC2_B, l, d, 0, d, d, true);
+      y.wgu = y.wd = -1;
+    } else {
+      y.wgu = add(CG_P_GATE_W, l, D.hid, d, d, (long long)D.Hp * d, true);
+      add(CG_P_UP_W, l, D.hid, d, d, (long long)D.Hp * d, false);
+      y.wd = add(CG_P_DOWN_W, l, d, D.hid, D.Hp, (long long)d * D.Hp, true);
+      y.w1 = y.b1 = y.w2 = y.b2 = -1;
+    }
+  }
+  Lo.lnfw = add(CG_P_LNF_W, -1, d, 0, d, d, true);
+  Lo.lnfb = add(CG_P_LNF_B, -1, d, 0, d, d, false);
+  if (!c->tie_embeddings) Lo.head = add(CG_P_HEAD_W, -1, D.V, d, d, (long long)D.Vp * d, true);
+  if (c->termination_aux) {
+    const int nc = c->termination_n_classes;
+    Lo.termw = add(CG_P_TERM_W, -1, nc, d, d, (long long)nc * d, true);
+    Lo.termb = add(CG_P_TERM_B, -1, nc, 0, nc, nc, true);
+  }
+  for (int i = 0; i < c->n_offsets && i < 8; ++i) {
+    Lo.off1w.push_back(add(CG_P_OFF1_W, i, d, d, d, (long long)d * d, true));
+    Lo.off1b.push_back(add(CG_P_OFF1_B, i, d, 0, d, d, true));
+    Lo.off2w.push_back(add(CG_P_OFF2_W, i, d, d, d, (long long)d * d, true));
+    Lo.off2b.push_back(add(CG_P_OFF2_B, i, d, 0, d, d, true));
+  }
+  Lo.total = rup(cur, ALIGN);
+}
+
+// ---------------------------------------------------------------------------
+// workspace carving
+// ---------------------------------------------------------------------------
+struct WS {
+  char* base = nullptr;
+  size_t off = 0;
+  template <typename P>
+  P* take(size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    P* p = base ? (P*)(base + off) : nullptr;
+    off += bytes;
+    return p;
+  }
+};
+
+struct LayerAct {
+  float *mean1, *rstd1, *mean2, *rstd2, *lse, *xmid;
+  void *h1, *qkv, *y, *h2, *a, *g, *gu, *s;
+};
+struct Acts {
+  int32_t* seg;
+  float* x;  // (L+1) x M x d
+  std::vector<LayerAct> la;
+  float *meanf, *rstdf, *logits_int;
+  void* xf;
+  // backward scratch
+  void *dlogits, *gT, *dbig, *dsmall;
+  float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
+  size_t splitws_floats;
+};
+
+constexpr int MAX_SPLIT = 8;
+
+size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Acts& A) {
+  WS w{base, 0};
+  const long long M = (long long)B * T;
+  const size_t es = c->dtype == CG_BF16 ? 2 : 4;
+  const int d = D.d;
+  A.seg = w.take<int32_t>(M * 4);
+  A.x = w.take<float>((size_t)(D.L + 1) * M * d * 4);
+  A.la.resize(D.L);
+  for (int l = 0; l < D.L; ++l) {
+    auto& a = A.la[l];
+    a.mean1 = w.take<float>(M * 4); a.rstd1 = w.take<float>(M * 4);
+    a.mean2 = w.take<float>(M * 4); a.rstd2 = w.take<float>(M * 4);
+    a.lse = w.take<float>((size_t)B * D.H * T * 4);
+    a.xmid = w.take<float>(M * d * 4);
+    a.h1 = w.take<char>(M * d * es);
+    a.qkv = w.take<char>(M * D.Nqkv * es);
+    a.y = w.take<char>(M * d * es);
+    a.h2 = w.take<char>(M * d * es);
+    if (!D.swiglu) {
+      a.a = w.take<char>(M * D.hid * es);
+      a.g = w.take<char>(M * D.hid * es);
+      a.gu = a.s = nullptr;
+    } else {
+      a.gu = w.take<char>(M * 2 * (size_t)D.Hp * es);
+      a.s = w.take<char>(M * (size_t)D.Hp * es);
+      a.a = a.g = nullptr;
+    }
+  }
+  A.meanf = w.take<float>(M * 4);
+  A.rstdf = w.take<float>(M * 4);
+  A.xf = w.take<char>(M * d * es);
+  A.logits_int = w.take<float>(M * D.V * 4);
+  A.dlogits = w.take<char>(M * D.Vp * es);
+  A.gT = w.take<char>(M * d * es);
+  const long long big = std::max<long long>({(long long)D.hid, 2LL * D.Hp, (long long)D.Nqkv});
+  A.dbig = w.take<char>(M * big * es);
+  A.dsmall = w.take<char>(M * std::max(d, D.Hp) * es);
+  A.g = w.take<float>(M * d * 4);
+  A.dtmp = w.take<float>(M * d * 4);
+  A.delta = w.take<float>((size_t)B * D.H * T * 4);
+  A.lnpart = w.take<float>((size_t)256 * 2 * d * 4);
+  const long long maxcols = std::max<long long>({big, (long long)d, (long long)D.Hp});
+  A.colws = w.take<float>((size_t)64 * maxcols * 4);
+  long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,
+                                        (long long)D.Vp * d, (long long)d * d});
+  A.splitws_floats = (size_t)MAX_SPLIT * wmax;
+  A.splitws = w.take<float>(A.splitws_floats * 4);
+  A.embws = w.take<float>((size_t)32 * D.V * d * 4);
+  A.cews = w.take<float>((size_t)(1 + 256) * 4);
+  return w.off + 256;
+}
+
+struct Ctx {
+  const cg_model* m;
+  Dims D;
+  Layout Lo;
+  Acts A;
+  int B, T;
+  long long M;
+  int dt;
+  hipStream_t s;
+};
+
+int make_ctx(const cg_model* m, int B, int T, void* stream, Ctx& C) {
+  if (!dims_of(&m->cfg, C.D)) return CG_EINVAL;
+  build_layout(&m->cfg, C.D, C.Lo);
+  C.m = m;
+  C.B = B; C.T = T; C.M = (long long)B * T;
+  C.dt = m->cfg.dtype;
+  C.s = (hipStream_t)stream;
+  size_t need = carve(&m->cfg, C.D, B, T, nullptr, C.A);
+  if (!m->workspace || m->workspace_bytes < need) return CG_EINVAL;
+  carve(&m->cfg, C.D, B, T, (char*)m->workspace, C.A);
+  return CG_OK;
+}
+
+inline const void* W(const Ctx& C, long long off) {
+  if (C.dt == CG_BF16) return (const void*)(C.m->shadow + off);
+  return (const void*)(C.m->params + off);
+}
+inline float* P(const Ctx& C, long long off) { return C.m->params + off; }
+inline float* G(const Ctx& C, long long off) { return C.m->grads + off; }
+inline size_t es(const Ctx& C) { return C.dt == CG_BF16 ? 2 : 4; }
+inline void* at(void* p, long long elems, const Ctx& C) { return (char*)p + elems * es(C); }
+
+#define CK(x)                      \
+  do {                             \
+    int _r = (x);                  \
+    if (_r != CG_OK) return _r;    \
+  } while (0)
+
+cg_gemm_desc gdesc(const Ctx& C) {
+  cg_gemm_desc g;
+  memset(&g, 0, sizeof(g));
+  g.in_dtype = C.dt;
+  g.c_dtype = C.dt;
+  g.alpha = 1.0f;
+  g.split_k = 1;
+  return g;
+}
+
+// y[M,N] = x[M,K] . W[N,K]^T  (forward nn.Linear)
+cg_gemm_desc lin_fwd(const Ctx& C, const void* x, long long ldx, long long woff, long long ldw, int N, int K, void* y,
+                     long long ldy) {
+  cg_gemm_desc g = gdesc(C);
+  g.M = (int)C.M; g.N = N; g.K = K;
+  g.A = x; g.lda = ldx; g.a_kcontig = 1;
+  g.B = W(C, woff); g.ldb = ldw; g.b_kcontig = 1;
+  g.C = y; g.ldc = ldy;
+  return g;
+}
+// dx[M,K] = dy[M,N] . W[N,K]
+cg_gemm_desc lin_dx(const Ctx& C, const void* dy, long long lddy, long long woff, long long ldw, int N, int K, void* dx,
+                    long long lddx) {
+  cg_gemm_desc g = gdesc(C);
+  g.M = (int)C.M; g.N = K; g.K = N;
+  g.A = dy; g.lda = lddy; g.a_kcontig = 1;
+  g.B = W(C, woff); g.ldb = ldw; g.b_kcontig = 0;
+  g.C = dx; g.ldc = lddx;
+  return g;
+}
+int pick_split(const Ctx& C, int Mo, int N, long long K) {
+  const int bm = C.dt == CG_BF16 ? 128 : 64;
+  const long long tiles = (long long)((Mo + bm - 1) / bm) * ((N + bm - 1) / bm);
+  long long s = (512 + tiles - 1) / tiles;
+  long long smax = K / 512;
+  if (s > smax) s = smax;
+  if (s > MAX_SPLIT) s = MAX_SPLIT;
+  if (s < 1) s = 1;
+  if ((size_t)s * Mo * N > C.A.splitws_floats) s = 1;
+  return (int)s;
+}
+// dW[N,K] (+)= dy[M,N]^T . x[M,K]
+int lin_dw(const Ctx& C, const void* dy, long long lddy, const void* x, long long ldx, int N, int K, long long goff,
+           long long ldg, int accumulate) {
+  cg_gemm_desc g = gdesc(C);
+  g.c_dtype = CG_F32;
+  g.M = N; g.N = K; g.K = (int)C.M;
+  g.A = dy; g.lda = lddy; g.a_kcontig = 0;
+  g.B = x; g.ldb = ldx; g.b_kcontig = 0;
+  g.C = G(C, goff); g.ldc = ldg;
+  g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
+  g.split_k = pick_split(C, N, K, C.M);
+  g.workspace = C.A.splitws;
+  return cg_gemm(&g, C.s);
+}
+int bias_grad(const Ctx& C, const void* dy, long long lddy, int N, long long goff, int accumulate) {
+  return cg_colsum(C.dt, dy, lddy, (int)C.M, N, G(C, goff), accumulate, C.A.colws, C.s);
+}
+
+float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
+
+}  // namespace
+
+// ===========================================================================
+extern "C" int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* out, int max, long long* total) {
+  Dims D;
+  if (!dims_of(cfg, D)) return CG_EINVAL;
+  Layout Lo;
+  build_layout(cfg, D, Lo);
+  if (total) *total = Lo.total;
+  const int n = (int)Lo.e.size();
+  if (out)
+    for (int i = 0; i < n && i < max; ++i) out[i] = Lo.e[i];
+  return n;
+}
+
+extern "C" size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T) {
+  Dims D;
+  if (!dims_of(cfg, D)) return 0;
+  Acts A;
+  return carve(cfg, D, B, T, nullptr, A);
+}
+
+extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, int B, int T, int training,
+                                uint32_t seed, int window, float* logits, float* loss, void* stream) {
+  if (!m || !idx || B <= 0 || T <= 0) return CG_EINVAL;
+  if (T > m->cfg.block_size) return CG_EINVAL;
+  if (m->cfg.dtype == CG_BF16 && !m->shadow) return CG_EINVAL;
+  if (m->cfg.use_rope && (!m->rope_cos || !m->rope_sin)) return CG_EINVAL;
+  m->B = B; m->T = T; m->training = training; m->seed = seed; m->window = window;
+  m->idx = idx; m->targets = targets;
+  Ctx C;
+  CK(make_ctx(m, B, T, stream, C));
+  const Dims& D = C.D;
+  const Acts& A = C.A;
+  const int d = D.d;
+  const long long M = C.M;
+  const float p = train_p(m);
+  const float eps = m->cfg.ln_eps > 0 ? m->cfg.ln_eps : 1e-5f;
+  m->logits = logits ? logits : A.logits_int;
+
+  CK(cg_segment_starts(idx, A.seg, B, T, m->cfg.sep_id, C.s));
+  CK(cg_embed_fwd(idx, P(C, C.Lo.tok), C.Lo.pos >= 0 ? P(C, C.Lo.pos) : nullptr, A.x, B, T, d,
+                  site_seed(seed, -1, SITE_EMB), p, C.s));
+  for (int l = 0; l < D.L; ++l) {
+    const auto& o = C.Lo.lay[l];
+    const auto& a = A.la[l];
+    float* xl = A.x + (size_t)l * M * d;
+    float* xn = A.x + (size_t)(l + 1) * M * d;
+    CK(cg_layernorm_fwd(C.dt, xl, d, P(C, o.ln1w), P(C, o.ln1b), a.h1, d, a.mean1, a.rstd1, (int)M, d, eps, C.s));
+    cg_gemm_desc g = lin_fwd(C, a.h1, d, o.wqkv, d, D.Nqkv, d, a.qkv, D.Nqkv);
+    g.epilogue = CG_EPI_BIAS; g.bias = P(C, o.bqkv);
+    CK(cg_gemm(&g, C.s));
+    if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
+    CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
+                   window, site_seed(seed, l, SITE_ATTN), p, C.s));
+    g = lin_fwd(C, a.y, d, o.wp, d, d, d, a.xmid, d);
+    g.c_dtype = CG_F32;
+    g.epilogue = CG_EPI_BIAS | CG_EPI_RESID; g.bias = P(C, o.bp); g.resid = xl; g.ldr = d;
+    CK(cg_gemm(&g, C.s));
+    CK(cg_layernorm_fwd(C.dt, a.xmid, d, P(C, o.ln2w), P(C, o.ln2b), a.h2, d, a.mean2, a.rstd2, (int)M, d, eps, C.s));
+    if (!D.swiglu) {
+      g = lin_fwd(C, a.h2, d, o.w1, d, D.hid, d, a.g, D.hid);
+      g.epilogue = CG_EPI_BIAS | CG_EPI_GELU; g.bias = P(C, o.b1); g.aux_out = a.a; g.ld_aux = D.hid;
+      CK(cg_gemm(&g, C.s));
+      g = lin_fwd(C, a.g, D.hid, o.w2, D.hid, d, D.hid, xn, d);
+      g.c_dtype = CG_F32;
+      g.epilogue = CG_EPI_BIAS | CG_EPI_RESID | (p > 0 ? CG_EPI_DROPOUT : 0);
+      g.bias = P(C, o.b2); g.resid = a.xmid; g.ldr = d;
+      g.drop_seed = site_seed(seed, l, SITE_MLP); g.drop_p = p;
+      CK(cg_gemm(&g, C.s));
+    } else {
+      g = lin_fwd(C, a.h2, d, o.wgu, d, 2 * D.Hp, d, a.gu, 2 * D.Hp);
+      CK(cg_gemm(&g, C.s));
+      CK(cg_swiglu_fwd(C.dt, a.gu, 2 * D.Hp, D.Hp, a.s, D.Hp, (int)M, D.hid, C.s));
+      g = lin_fwd(C, a.s, D.Hp, o.wd, D.Hp, d, D.Hp, xn, d);
+      g.c_dtype = CG_F32;
+      g.epilogue = CG_EPI_RESID | (p > 0 ? CG_EPI_DROPOUT : 0);
+      g.resid = a.xmid; g.ldr = d;
+      g.drop_seed = site_seed(seed, l, SITE_MLP); g.drop_p = p;
+      CK(cg_gemm(&g, C.s));
+    }
+  }
+  float* xL = A.x + (size_t)D.L * M * d;
+  CK(cg_layernorm_fwd(C.dt, xL, d, P(C, C.Lo.lnfw), P(C, C.Lo.lnfb), A.xf, d, A.meanf, A.rstdf, (int)M, d, eps, C.s));
+  const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+  cg_gemm_desc g = lin_fwd(C, A.xf, d, hoff, d, D.V, d, m->logits, D.V);
+  g.c_dtype = CG_F32;
+  CK(cg_gemm(&g, C.s));
+  if (targets) {
+    CK(cg_cross_entropy(m->logits, D.V, targets, (int)M, D.V, m->cfg.label_smoothing, m->loss_weights, 0, 1.0f, C.dt,
+                        A.dlogits, D.Vp, loss, A.cews, C.s));
+  }
+  return CG_OK;
+}
+
+extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* stream) {
+  if (!m || !m->idx || !m->grads) return CG_EINVAL;
+  if (!m->targets) return CG_EINVAL;
+  Ctx C;
+  CK(make_ctx(m, m->B, m->T, stream, C));
+  const Dims& D = C.D;
+  const Acts& A = C.A;
+  const int d = D.d;
+  const long long M = C.M;
+  const float p = train_p(m);
+  const float eps = m->cfg.ln_eps > 0 ? m->cfg.ln_eps : 1e-5f;
+  const uint32_t seed = m->seed;
+
+  if (phase == 0) {
+    const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+    // d(head weight) = dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero)
+    cg_gemm_desc g = gdesc(C);
+    g.c_dtype = CG_F32;
+    g.M = D.Vp; g.N = d; g.K = (int)M;
+    g.A = A.dlogits; g.lda = D.Vp; g.a_kcontig = 0;
+    g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
+    g.C = G(C, hoff); g.ldc = d;
+    g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
+    g.split_k = pick_split(C, D.Vp, d, M);
+    g.workspace = A.splitws;
+    CK(cg_gemm(&g, C.s));
+    // dxf = dlogits . E
+    g = lin_dx(C, A.dlogits, D.Vp, hoff, d, D.Vp, d, A.dtmp, d);
+    g.c_dtype = CG_F32;
+    CK(cg_gemm(&g, C.s));
+    float* xL = A.x + (size_t)D.L * M * d;
+    const int ll = D.L - 1;
+    CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xL, d, A.meanf, A.rstdf, P(C, C.Lo.lnfw), nullptr, A.g, C.dt,
+                        D.L > 0 ? A.gT : nullptr, site_seed(seed, ll, SITE_MLP), D.L > 0 ? p : 0.f, A.lnpart,
+                        G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), accumulate, (int)M, d, eps, C.s));
+    return CG_OK;
+  }
+  if (phase == 1) {
+    const int l = layer;
+    if (l < 0 || l >= D.L) return CG_EINVAL;
+    const auto& o = C.Lo.lay[l];
+    const auto& a = A.la[l];
+    float* xl = A.x + (size_t)l * M * d;
+    // ---------------- MLP branch: gT = dL/d(mlp out) (dropout mask applied)
+    if (!D.swiglu) {
+      CK(lin_dw(C, A.gT, d, a.g, D.hid, d, D.hid, o.w2, D.hid, accumulate));
+      CK(bias_grad(C, A.gT, d, d, o.b2, accumulate));
+      cg_gemm_desc g = lin_dx(C, A.gT, d, o.w2, D.hid, d, D.hid, A.dbig, D.hid);
+      g.epilogue = CG_EPI_DGELU; g.aux = a.a; g.ld_aux = D.hid;
+      CK(cg_gemm(&g, C.s));
+      CK(lin_dw(C, A.dbig, D.hid, a.h2, d, D.hid, d, o.w1, d, accumulate));
+      CK(bias_grad(C, A.dbig, D.hid, D.hid, o.b1, accumulate));
+      g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dtmp, d);
+      g.c_dtype = CG_F32;
+      CK(cg_gemm(&g, C.s));
+    } else {
+      CK(lin_dw(C, A.gT, d, a.s, D.Hp, d, D.Hp, o.wd, D.Hp, accumulate));
+      cg_gemm_desc g = lin_dx(C, A.gT, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp);
+      CK(cg_gemm(&g, C.s));
+      CK(cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, A.dbig, 2 * D.Hp, (int)M, D.hid, C.s));
+      CK(lin_dw(C, A.dbig, 2 * D.Hp, a.h2, d, 2 * D.Hp, d, o.wgu, d, accumulate));
+      g = lin_dx(C, A.dbig, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dtmp, d);
+      g.c_dtype = CG_F32;
+      CK(cg_gemm(&g, C.s));
+    }
+    CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, A.gT, 0, 0.f,
+                        A.lnpart, G(C, o.ln2w), G(C, o.ln2b), accumulate, (int)M, d, eps, C.s));
+    // ---------------- attention branch: gT = dL/d(proj out)
+    CK(lin_dw(C, A.gT, d, a.y, d, d, d, o.wp, d, accumulate));
+    CK(bias_grad(C, A.gT, d, d, o.bp, accumulate));
+    cg_gemm_desc g = lin_dx(C, A.gT, d, o.wp, d, d, d, A.dsmall, d);
+    CK(cg_gemm(&g, C.s));
+    CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, A.dbig,
+                   D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, A.delta, C.s));
+    if (D.rope)
+      CK(cg_rope_tab(C.dt, A.dbig, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
+    CK(lin_dw(C, A.dbig, D.Nqkv, a.h1, d, D.Nqkv, d, o.wqkv, d, accumulate));
+    CK(bias_grad(C, A.dbig, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
+    g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dtmp, d);
+    g.c_dtype = CG_F32;
+    CK(cg_gemm(&g, C.s));
+    CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xl, d, a.mean1, a.rstd1, P(C, o.ln1w), A.g, A.g, C.dt,
+                        l > 0 ? A.gT : nullptr, site_seed(seed, l - 1, SITE_MLP), l > 0 ? p : 0.f, A.lnpart,
+                        G(C, o.ln1w), G(C, o.ln1b), accumulate, (int)M, d, eps, C.s));
+    return CG_OK;
+  }
+  if (phase == 2) {
+    // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
+    const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
+    CK(cg_embed_bwd(m->idx, A.g, G(C, C.Lo.tok), nullptr, C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
+                    acc_tok, A.embws, C.s));
+    if (C.Lo.pos >= 0)
+      CK(cg_embed_bwd(m->idx, A.g, nullptr, G(C, C.Lo.pos), C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
+                      accumulate, A.embws, C.s));
+    return CG_OK;
+  }
+  return CG_EINVAL;
+}
+
+extern "C" const void* cg_model_hidden(const cg_model* m, int which, int* dtype_out, long long* ld) {
+  if (!m) return nullptr;
+  Ctx C;
+  if (make_ctx(m, m->B, m->T, nullptr, C) != CG_OK) return nullptr;
+  const long long M = C.M;
+  if (ld) *ld = C.D.d;
+  if (which >= 0 && which <= C.D.L) {
+    if (dtype_out) *dtype_out = CG_F32;
+    return C.A.x + (size_t)which * M * C.D.d;
+  }
+  if (which == C.D.L + 1) {
+    if (dtype_out) *dtype_out = C.dt;
+    return C.A.xf;
+  }
+  return nullptr;
+}
+
+extern "C" const char* cg_version(void) { return "codonlm_hip 0.1 gfx950"; }

@@ -1,0 +1,720 @@
+// Memory-bound kernels of the TinyGPT step: LayerNorm fwd/bwd, embedding fwd/bwd,
+// SEP segment starts, RoPE, SwiGLU, bias column sums, label-smoothed CE, AdamW,
+// casts.  All are HBM-bound; rows are processed one 64-lane wave per row with
+// coalesced lane-strided access, cross-row reductions go through per-block partial
+// slabs reduced in a fixed order (bitwise reproducible, no float atomics).
+#include "common.h"
+
+// ===========================================================================
+// LayerNorm  (nn.LayerNorm(d), eps=1e-5, biased variance; model_tiny_gpt.py:137-152,216)
+// ===========================================================================
+constexpr int LN_MAXV = 32;  // cols <= 2048
+
+template <typename TO>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, long long ldx,
+                                                     const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, TO* __restrict__ y,
+                                                     long long ldy, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, int rows, int cols, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * ldx;
+  float v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = (c < cols) ? xr[c] : 0.f;
+    s += v[i];
+  }
+  const float mu = wave_sum(s) / (float)cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    const float dlt = (c < cols) ? v[i] - mu : 0.f;
+    q += dlt * dlt;
+  }
+  const float var = wave_sum(q) / (float)cols;
+  const float rs = rsqrtf(var + eps);
+  TO* yr = y + (long long)row * ldy;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < cols) st_act<TO>(yr + c, (v[i] - mu) * rs * gamma[c] + beta[c]);
+  }
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = rs;
+  }
+}
+
+extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,
+                                const float* beta, void* y, long long ldy, float* mean, float* rstd,
+                                int rows, int cols, float eps, void* stream) {
+  if (cols <= 0 || cols > 64 * LN_MAXV || rows < 0) return CG_EUNSUPPORTED;
+  if (rows == 0) return CG_OK;
+  dim3 g(cg_cdiv(rows, 4));
+  if (out_dtype == CG_BF16)
+    hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, x, ldx, gamma, beta,
+                       (bf16_t*)y, ldy, mean, rstd, rows, cols, eps);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, x, ldx, gamma, beta,
+                       (float*)y, ldy, mean, rstd, rows, cols, eps);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+extern "C" int cg_layernorm_bwd_blocks(int rows) {
+  int b = cg_cdiv(rows, 4);
+  return b > 256 ? 256 : (b < 1 ? 1 : b);
+}
+
+// dx = rstd * (dy*g - mean(dy*g) - xhat*mean(dy*g*xhat));  g_out = g_in + dx
+template <typename TD, typename TO>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, long long lddy,
+                                                     const float* __restrict__ x, long long ldx,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const float* __restrict__ gamma, const float* __restrict__ g_in,
+                                                     float* __restrict__ g_out, TO* __restrict__ g_out_t,
+                                                     uint32_t seed, uint32_t thr, float dscale,
+                                                     float* __restrict__ partials, int rows, int cols) {
+  __shared__ float red[4][2 * 64 * 8];  // per-wave column partials, chunked
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int rows_per_blk = (rows + gridDim.x - 1) / gridDim.x;
+  const int r_begin = blockIdx.x * rows_per_blk;
+  const int r_end = min(rows, r_begin + rows_per_blk);
+  float dg[LN_MAXV], db[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) { dg[i] = 0.f; db[i] = 0.f; }
+  for (int row = r_begin + wave; row < r_end; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    const float* xr = x + (long long)row * ldx;
+    const TD* dyr = dy + (long long)row * lddy;
+    float xh[LN_MAXV], gy[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < cols) {
+        const float d = ld_act<TD>(dyr + c);
+        xh[i] = (xr[c] - mu) * rs;
+        gy[i] = d * gamma[c];
+        dg[i] += d * xh[i];
+        db[i] += d;
+      } else {
+        xh[i] = 0.f; gy[i] = 0.f;
+      }
+      s1 += gy[i];
+      s2 += gy[i] * xh[i];
+    }
+    s1 = wave_sum(s1) / (float)cols;
+    s2 = wave_sum(s2) / (float)cols;
+    const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
+    float* go = g_out + (long long)row * cols;
+    TO* got = g_out_t ? g_out_t + (long long)row * cols : nullptr;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < cols) {
+        float v = rs * (gy[i] - s1 - xh[i] * s2);
+        if (gi) v += gi[c];
+        go[c] = v;
+        if (got) {
+          float w = v;
+          if (thr) w = cg_keep(seed, (uint32_t)row, (uint32_t)c, thr) ? w * dscale : 0.f;
+          st_act<TO>(got + c, w);
+        }
+      }
+    }
+  }
+  // reduce the 4 waves' column partials in fixed order, 64*8 columns at a time
+#pragma unroll
+  for (int cb = 0; cb < LN_MAXV; cb += 8) {
+    if (cb * 64 >= cols) continue;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[wave][i * 64 + lane] = dg[cb + i];
+      red[wave][512 + i * 64 + lane] = db[cb + i];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 1024; e += 256) {
+      const int which = e >> 9, rem = e & 511, i = rem >> 6, l = rem & 63;
+      const int c = l + 64 * (cb + i);
+      if (c < cols) {
+        const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+        partials[(long long)blockIdx.x * 2 * cols + which * cols + c] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void ln_param_reduce_kernel(const float* __restrict__ partials, int nblk, int cols,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partials[(long long)b * 2 * cols + c];
+  float* dst = c < cols ? dgamma + c : dbeta + (c - cols);
+  *dst = accumulate ? *dst + s : s;
+}
+
+extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
+                                const float* mean, const float* rstd, const float* gamma, const float* g_in,
+                                float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
+                                float* partials, float* dgamma, float* dbeta, int accumulate, int rows,
+                                int cols, float eps, void* stream) {
+  (void)eps;
+  if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
+  if (rows <= 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = cg_layernorm_bwd_blocks(rows);
+  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
+  const float dscale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+#define LNB(TD, TO)                                                                                  \
+  hipLaunchKernelGGL((ln_bwd_kernel<TD, TO>), dim3(nblk), dim3(256), 0, s, (const TD*)dy, lddy, x, ldx, \
+                     mean, rstd, gamma, g_in, g_out, (TO*)g_out_t, drop_seed, thr, dscale, partials, rows, cols)
+  if (dy_dtype == CG_BF16) {
+    if (out_dtype == CG_BF16) LNB(bf16_t, bf16_t); else LNB(bf16_t, float);
+  } else {
+    if (out_dtype == CG_BF16) LNB(float, bf16_t); else LNB(float, float);
+  }
+#undef LNB
+  CG_LAUNCH_CHECK();
+  if (dgamma && dbeta) {
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cg_cdiv(2 * cols, 256)), dim3(256), 0, s, partials, nblk,
+                       cols, dgamma, dbeta, accumulate);
+    CG_LAUNCH_CHECK();
+  }
+  return CG_OK;
+}
+
+// ===========================================================================
+// Embedding (model_tiny_gpt.py:305-312)
+// ===========================================================================
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ idx, const float* __restrict__ tok,
+                                                        const float* __restrict__ pos, float* __restrict__ x,
+                                                        int B, int T, int d, uint32_t seed, uint32_t thr, float dscale) {
+  const long long total = (long long)B * T * d;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long m = e / d;
+    const int c = (int)(e - m * d);
+    const int t = (int)(m % T);
+    float v = tok[idx[m] * d + c];
+    if (pos) v += pos[(long long)t * d + c];
+    if (thr) v = cg_keep(seed, (uint32_t)m, (uint32_t)c, thr) ? v * dscale : 0.f;
+    x[e] = v;
+  }
+}
+
+extern "C" int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const float* pos_emb, float* x, int B,
+                            int T, int d, uint32_t drop_seed, float drop_p, void* stream) {
+  const long long total = (long long)B * T * d;
+  if (total == 0) return CG_OK;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx, tok_emb, pos_emb, x,
+                     B, T, d, drop_seed, thr, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+constexpr int EMB_RCHUNKS = 32;
+extern "C" size_t cg_embed_bwd_workspace(int B, int T, int V, int d) {
+  (void)B; (void)T;
+  return (size_t)EMB_RCHUNKS * V * d * sizeof(float);
+}
+
+// per (64-column chunk, row chunk): each wave accumulates its own rows into its own LDS
+// [V][64] slab (no atomics), the 4 slabs are summed in order into a global partial slab.
+__global__ __launch_bounds__(256) void embed_bwd_tok_kernel(const int64_t* __restrict__ idx, const float* __restrict__ g,
+                                                            float* __restrict__ part, int rows, int V, int d,
+                                                            uint32_t seed, uint32_t thr, float dscale) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];  // [4][V][64]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  for (int e = threadIdx.x; e < 4 * V * 64; e += 256) acc[e] = 0.f;
+  __syncthreads();
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float* mine = acc + wave * V * 64;
+  if (c < d) {
+    for (int r = r0 + wave; r < r1; r += 4) {
+      const int tkn = (int)idx[r];
+      float v = g[(long long)r * d + c];
+      if (thr) v = cg_keep(seed, (uint32_t)r, (uint32_t)c, thr) ? v * dscale : 0.f;
+      mine[tkn * 64 + lane] += v;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < V * 64; e += 256) {
+    const int v = e >> 6, l = e & 63, cc = blockIdx.x * 64 + l;
+    if (cc < d) {
+      const float s = acc[e] + acc[V * 64 + e] + acc[2 * V * 64 + e] + acc[3 * V * 64 + e];
+      part[((long long)blockIdx.y * V + v) * d + cc] = s;
+    }
+  }
+}
+
+__global__ void embed_bwd_tok_reduce(const float* __restrict__ part, float* __restrict__ dtok, int nch, int V, int d,
+                                     int accumulate) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= V * d) return;
+  float s = 0.f;
+  for (int ch = 0; ch < nch; ++ch) s += part[(long long)ch * V * d + e];
+  dtok[e] = accumulate ? dtok[e] + s : s;
+}
+
+__global__ void embed_bwd_pos_kernel(const float* __restrict__ g, float* __restrict__ dpos, int B, int T, int d,
+                                     uint32_t seed, uint32_t thr, float dscale, int accumulate) {
+  const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (e >= (long long)T * d) return;
+  const int t = (int)(e / d), c = (int)(e % d);
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const long long m = (long long)b * T + t;
+    float v = g[m * d + c];
+    if (thr) v = cg_keep(seed, (uint32_t)m, (uint32_t)c, thr) ? v * dscale : 0.f;
+    s += v;
+  }
+  dpos[e] = accumulate ? dpos[e] + s : s;
+}
+
+extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, float* dpos, int B, int T, int V,
+                            int d, uint32_t drop_seed, float drop_p, int accumulate, void* ws, void* stream) {
+  if (V > 256) return CG_EUNSUPPORTED;
+  const int rows = B * T;
+  if (rows == 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
+  const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
+  if (dtok) {
+    int nch = EMB_RCHUNKS;
+    if (nch > rows) nch = rows;
+    const size_t sh = (size_t)4 * V * 64 * sizeof(float);
+    if (sh > 160 * 1024) return CG_EUNSUPPORTED;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)embed_bwd_tok_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(embed_bwd_tok_kernel, dim3(cg_cdiv(d, 64), nch), dim3(256), sh, s, idx, g, (float*)ws, rows,
+                       V, d, drop_seed, thr, dscale);
+    CG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(embed_bwd_tok_reduce, dim3(cg_cdiv(V * d, 256)), dim3(256), 0, s, (const float*)ws, dtok,
+                       nch, V, d, accumulate);
+    CG_LAUNCH_CHECK();
+  }
+  if (dpos) {
+    hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(cg_cdiv((long long)T * d, 256)), dim3(256), 0, s, g, dpos, B, T,
+                       d, drop_seed, thr, dscale, accumulate);
+    CG_LAUNCH_CHECK();
+  }
+  return CG_OK;
+}
+
+// ===========================================================================
+// SEP segment starts: segstart[b,t] = max{p <= t : idx[b,p] == sep} (0 if none)
+// (same-segment test of build_attention_mask, model_tiny_gpt.py:289-294)
+// ===========================================================================
+__global__ __launch_bounds__(256) void segstart_kernel(const int64_t* __restrict__ idx, int32_t* __restrict__ out,
+                                                       int T, int sep) {
+  __shared__ int tot[256];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int per = (T + 255) / 256;
+  const int t0 = tid * per, t1 = min(T, t0 + per);
+  int run = 0;
+  for (int t = t0; t < t1; ++t)
+    if (sep >= 0 && idx[(long long)b * T + t] == sep) run = t;
+  tot[tid] = run;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    int v = (tid >= off) ? tot[tid - off] : 0;
+    __syncthreads();
+    tot[tid] = max(tot[tid], v);
+    __syncthreads();
+  }
+  run = tid > 0 ? tot[tid - 1] : 0;
+  for (int t = t0; t < t1; ++t) {
+    if (sep >= 0 && idx[(long long)b * T + t] == sep) run = t;
+    out[(long long)b * T + t] = run;
+  }
+}
+
+extern "C" int cg_segment_starts(const int64_t* idx, int32_t* segstart, int B, int T, int sep_id, void* stream) {
+  if (B == 0 || T == 0) return CG_OK;
+  hipLaunchKernelGGL(segstart_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, idx, segstart, T, sep_id);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// RoPE in place on packed qkv rows (rotate_half form; model_tiny_gpt.py:35-45)
+// cos/sin tables [T][hd/2] are built on the host exactly like RotaryEmbedding.
+// ===========================================================================
+template <typename T_>
+__global__ __launch_bounds__(256) void rope_kernel(T_* __restrict__ qkv, long long ld, int rows, int T, int nh, int hd,
+                                                   const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                   int inverse) {
+  const int half = hd >> 1;
+  const long long total = (long long)rows * nh * half;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int i = (int)(e % half);
+    const long long rh = e / half;
+    const int h = (int)(rh % nh);
+    const long long m = rh / nh;
+    const int t = (int)(m % T);
+    T_* base = qkv + m * ld + (long long)h * hd;
+    const float x1 = ld_act<T_>(base + i), x2 = ld_act<T_>(base + i + half);
+    const float c = cosb[(long long)t * half + i], s = sinb[(long long)t * half + i];
+    float y1, y2;
+    if (!inverse) { y1 = x1 * c - x2 * s; y2 = x2 * c + x1 * s; }
+    else          { y1 = x1 * c + x2 * s; y2 = x2 * c - x1 * s; }
+    st_act<T_>(base + i, y1);
+    st_act<T_>(base + i + half, y2);
+  }
+}
+
+extern "C" int cg_rope_tab(int dtype, void* qkv, long long ldqkv, int B, int T, int H, int KV, int hd,
+                           const float* cos_tab, const float* sin_tab, int inverse, void* stream) {
+  if (hd & 1) return CG_EUNSUPPORTED;
+  const int rows = B * T, nh = H + KV;  // q heads then k heads are contiguous column blocks
+  const long long total = (long long)rows * nh * (hd / 2);
+  if (total == 0) return CG_OK;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(rope_kernel<bf16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (bf16_t*)qkv, ldqkv,
+                       rows, T, nh, hd, cos_tab, sin_tab, inverse);
+  else
+    hipLaunchKernelGGL(rope_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (float*)qkv, ldqkv,
+                       rows, T, nh, hd, cos_tab, sin_tab, inverse);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// SwiGLU (model_tiny_gpt.py:47-57): s = silu(g) * u, gate at cols [0,H), up at [Hp,Hp+H)
+// ===========================================================================
+template <typename T_>
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const T_* __restrict__ gu, long long ldgu, int Hp,
+                                                         T_* __restrict__ s, long long lds, int rows, int H) {
+  const long long total = (long long)rows * Hp;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long m = e / Hp;
+    const int j = (int)(e - m * Hp);
+    float v = 0.f;
+    if (j < H) {
+      const float g = ld_act<T_>(gu + m * ldgu + j), u = ld_act<T_>(gu + m * ldgu + Hp + j);
+      v = silu_f(g) * u;
+    }
+    st_act<T_>(s + m * lds + j, v);
+  }
+}
+template <typename T_>
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const T_* __restrict__ gu, long long ldgu, int Hp,
+                                                         const T_* __restrict__ ds, long long ldds,
+                                                         T_* __restrict__ dgu, long long lddgu, int rows, int H) {
+  const long long total = (long long)rows * Hp;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long m = e / Hp;
+    const int j = (int)(e - m * Hp);
+    float dg = 0.f, du = 0.f;
+    if (j < H) {
+      const float g = ld_act<T_>(gu + m * ldgu + j), u = ld_act<T_>(gu + m * ldgu + Hp + j);
+      const float d = ld_act<T_>(ds + m * ldds + j);
+      const float sg = 1.0f / (1.0f + __expf(-g));
+      const float sl = g * sg;
+      du = d * sl;
+      dg = d * u * sg * (1.0f + g * (1.0f - sg));
+    }
+    st_act<T_>(dgu + m * lddgu + j, dg);
+    st_act<T_>(dgu + m * lddgu + Hp + j, du);
+  }
+}
+
+extern "C" int cg_swiglu_fwd(int dtype, const void* gu, long long ldgu, int Hp, void* s, long long lds, int rows,
+                             int H, void* stream) {
+  const long long total = (long long)rows * Hp;
+  if (total == 0) return CG_OK;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(swiglu_fwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)gu, ldgu, Hp, (bf16_t*)s, lds, rows, H);
+  else
+    hipLaunchKernelGGL(swiglu_fwd_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float*)gu,
+                       ldgu, Hp, (float*)s, lds, rows, H);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+extern "C" int cg_swiglu_bwd(int dtype, const void* gu, long long ldgu, int Hp, const void* ds, long long ldds,
+                             void* dgu, long long lddgu, int rows, int H, void* stream) {
+  const long long total = (long long)rows * Hp;
+  if (total == 0) return CG_OK;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(swiglu_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                       (const bf16_t*)gu, ldgu, Hp, (const bf16_t*)ds, ldds, (bf16_t*)dgu, lddgu, rows, H);
+  else
+    hipLaunchKernelGGL(swiglu_bwd_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const float*)gu,
+                       ldgu, Hp, (const float*)ds, ldds, (float*)dgu, lddgu, rows, H);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// Column sums for bias gradients: out[n] (+)= sum_m X[m, n]
+// ===========================================================================
+constexpr int COLSUM_R = 64;
+extern "C" size_t cg_colsum_workspace(int rows, int cols) {
+  (void)rows;
+  return (size_t)COLSUM_R * cols * sizeof(float);
+}
+template <typename T_>
+__global__ __launch_bounds__(256) void colsum_part_kernel(const T_* __restrict__ X, long long ldx, int rows, int cols,
+                                                          float* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += ld_act<T_>(X + (long long)r * ldx + c);
+  part[(long long)blockIdx.y * cols + c] = s;
+}
+__global__ void colsum_reduce_kernel(const float* __restrict__ part, int nch, int cols, float* __restrict__ out,
+                                     int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int i = 0; i < nch; ++i) s += part[(long long)i * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
+}
+extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out, int accumulate,
+                         void* ws, void* stream) {
+  if (cols == 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  int nch = COLSUM_R;
+  if (nch > rows) nch = rows > 0 ? rows : 1;
+  dim3 g(cg_cdiv(cols, 256), nch);
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(colsum_part_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)X, ldx, rows, cols, (float*)ws);
+  else
+    hipLaunchKernelGGL(colsum_part_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, (float*)ws);
+  CG_LAUNCH_CHECK();
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 256)), dim3(256), 0, s, (const float*)ws, nch, cols, out,
+                     accumulate);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// Cross-entropy: label smoothing + class weights + ignore_index (F.cross_entropy,
+// model_tiny_gpt.py:343-349). L = sum_valid[(1-e) w_y nll_y + e/V sum_c w_c nll_c] / sum_valid w_y
+// ===========================================================================
+constexpr int CE_BLK = 256;   // rows per block = 4 waves x 1 row, grid-strided
+__global__ __launch_bounds__(1024) void ce_denom_kernel(const int64_t* __restrict__ tg, int rows, const float* __restrict__ w,
+                                                        int ignore, float* __restrict__ ws) {
+  __shared__ float red[1024];
+  float s = 0.f;
+  for (int r = threadIdx.x; r < rows; r += 1024) {
+    const int64_t t = tg[r];
+    if (t != ignore) s += w ? w[t] : 1.0f;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ws[0] = red[0];
+}
+
+template <typename TD>
+__global__ __launch_bounds__(256) void ce_main_kernel(const float* __restrict__ logits, long long ldl,
+                                                      const int64_t* __restrict__ tg, int rows, int V, float eps,
+                                                      const float* __restrict__ w, int ignore, float grad_scale,
+                                                      TD* __restrict__ dl, long long ldd, float* __restrict__ ws) {
+  __shared__ float wsum[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float denom = ws[0];
+  const float inv = grad_scale / denom;
+  float acc = 0.f;
+  // total class weight W
+  float Wt = 0.f;
+  for (int c = lane; c < V; c += 64) Wt += w ? w[c] : 1.0f;
+  Wt = wave_sum(Wt);
+  for (int row = blockIdx.x * 4 + wave; row < rows; row += gridDim.x * 4) {
+    const float* z = logits + (long long)row * ldl;
+    const int64_t t = tg[row];
+    const bool valid = (t != ignore);
+    float z0 = lane < V ? z[lane] : -INFINITY;
+    float z1 = (lane + 64) < V ? z[lane + 64] : -INFINITY;
+    const float mx = wave_max(fmaxf(z0, z1));
+    float e0 = lane < V ? __expf(z0 - mx) : 0.f;
+    float e1 = (lane + 64) < V ? __expf(z1 - mx) : 0.f;
+    const float se = wave_sum(e0 + e1);
+    const float lse = mx + __logf(se);
+    TD* dr = dl ? dl + (long long)row * ldd : nullptr;
+    if (valid) {
+      const float wy = w ? w[t] : 1.0f;
+      // smoothing term sum_c w_c (lse - z_c)
+      float sm = 0.f;
+      if (lane < V) sm += (w ? w[lane] : 1.f) * (lse - z0);
+      if (lane + 64 < V) sm += (w ? w[lane + 64] : 1.f) * (lse - z1);
+      sm = wave_sum(sm);
+      const float zy = z[t];
+      acc += (1.0f - eps) * wy * (lse - zy) + (eps / (float)V) * sm;
+      if (dr) {
+        const float rse = 1.0f / se;
+        for (int k = 0; k < 2; ++k) {
+          const int c = lane + 64 * k;
+          if (c < V) {
+            const float p = (k == 0 ? e0 : e1) * rse;
+            const float wc = w ? w[c] : 1.f;
+            float g = (1.0f - eps) * wy * (p - (c == t ? 1.f : 0.f)) + (eps / (float)V) * (Wt * p - wc);
+            st_act<TD>(dr + c, g * inv);
+          }
+        }
+      }
+    } else if (dr) {
+      for (int c = lane; c < V; c += 64) st_act<TD>(dr + c, 0.f);
+    }
+    if (dr)
+      for (int c = V + lane; c < ldd; c += 64) st_act<TD>(dr + c, 0.f);
+  }
+  if (lane == 0) wsum[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) ws[1 + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ void ce_final_kernel(const float* __restrict__ ws, int nblk, float* __restrict__ loss) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += ws[1 + b];
+    *loss = s / ws[0];
+  }
+}
+
+static int ce_blocks(int rows) {
+  int b = cg_cdiv(rows, 4);
+  return b > CE_BLK ? CE_BLK : (b < 1 ? 1 : b);
+}
+extern "C" size_t cg_ce_workspace(int rows) { return (size_t)(1 + ce_blocks(rows)) * sizeof(float); }
+
+extern "C" int cg_cross_entropy(const float* logits, long long ldl, const int64_t* targets, int rows, int V,
+                                float eps, const float* class_w, int ignore_index, float grad_scale, int d_dtype,
+                                void* dlogits, long long ldd, float* loss, void* ws, void* stream) {
+  if (V > 128 || V <= 0) return CG_EUNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = ce_blocks(rows);
+  hipLaunchKernelGGL(ce_denom_kernel, dim3(1), dim3(1024), 0, s, targets, rows, class_w, ignore_index, (float*)ws);
+  CG_LAUNCH_CHECK();
+  if (d_dtype == CG_BF16)
+    hipLaunchKernelGGL(ce_main_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, logits, ldl, targets, rows, V, eps,
+                       class_w, ignore_index, grad_scale, (bf16_t*)dlogits, ldd, (float*)ws);
+  else
+    hipLaunchKernelGGL(ce_main_kernel<float>, dim3(nblk), dim3(256), 0, s, logits, ldl, targets, rows, V, eps,
+                       class_w, ignore_index, grad_scale, (float*)dlogits, ldd, (float*)ws);
+  CG_LAUNCH_CHECK();
+  if (loss) {
+    hipLaunchKernelGGL(ce_final_kernel, dim3(1), dim3(64), 0, s, (const float*)ws, nblk, loss);
+    CG_LAUNCH_CHECK();
+  }
+  return CG_OK;
+}
+
+// ===========================================================================
+// AdamW over the flat parameter buffer (torch.optim.AdamW, loop.py:681-731)
+// ===========================================================================
+struct AdamSegs { long long begin[4], end[4]; float lr[4], wd[4]; int n; };
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                    float* __restrict__ m, float* __restrict__ v,
+                                                    bf16_t* __restrict__ shadow, AdamSegs segs, float b1, float b2,
+                                                    float eps, float bc1, float bc2_sqrt, float gscale) {
+  for (int si = 0; si < segs.n; ++si) {
+    const long long b = segs.begin[si], e = segs.end[si];
+    const float lr = segs.lr[si], wd = segs.wd[si];
+    const float step_size = lr / bc1;
+    for (long long i = b + blockIdx.x * 256ll + threadIdx.x; i < e; i += (long long)gridDim.x * 256) {
+      const float gi = g[i] * gscale;
+      float pi = p[i] * (1.0f - lr * wd);
+      const float mi = b1 * m[i] + (1.0f - b1) * gi;
+      const float vi = b2 * v[i] + (1.0f - b2) * gi * gi;
+      m[i] = mi;
+      v[i] = vi;
+      const float denom = sqrtf(vi) / bc2_sqrt + eps;
+      pi = pi - step_size * (mi / denom);
+      p[i] = pi;
+      if (shadow) shadow[i] = f2bf(pi);
+    }
+  }
+}
+
+extern "C" int cg_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, uint16_t* shadow_bf16,
+                        const cg_adamw_segment* segs, int nseg, float beta1, float beta2, float eps, int step,
+                        float grad_scale, void* stream) {
+  if (nseg < 1 || nseg > 4 || step < 1) return CG_EINVAL;
+  AdamSegs s{};
+  long long total = 0;
+  for (int i = 0; i < nseg; ++i) {
+    s.begin[i] = segs[i].begin; s.end[i] = segs[i].end; s.lr[i] = segs[i].lr; s.wd[i] = segs[i].wd;
+    total += segs[i].end - segs[i].begin;
+  }
+  s.n = nseg;
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
+                     (bf16_t*)shadow_bf16, s, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), grad_scale);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+__global__ void nonfinite_kernel(const float* __restrict__ x, long long n, int* __restrict__ flag) {
+  int bad = 0;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    bad |= !isfinite(x[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+extern "C" int cg_nonfinite_flag(const float* x, long long n, int* flag, void* stream) {
+  if (n <= 0) return CG_OK;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(nonfinite_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, x, n, flag);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// casts
+// ===========================================================================
+__global__ void cast_f2b_kernel(const float* __restrict__ s, bf16_t* __restrict__ d, long long n) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) d[i] = f2bf(s[i]);
+}
+__global__ void cast_b2f_kernel(const bf16_t* __restrict__ s, float* __restrict__ d, long long n) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) d[i] = bf2f(s[i]);
+}
+extern "C" int cg_cast_f32_to_bf16(const float* src, uint16_t* dst, long long n, void* stream) {
+  if (n <= 0) return CG_OK;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cast_f2b_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, (bf16_t*)dst, n);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+extern "C" int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stream) {
+  if (n <= 0) return CG_OK;
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(cast_b2f_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src, dst, n);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}

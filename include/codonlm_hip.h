@@ -1,0 +1,218 @@
+/*
+ * codonlm_hip.h -- C-ABI of the MI355X-native codon-LM hot path (libcodonlm_hip.so).
+ *
+ * The reference (AvishaiBarnoy/genomics-lm) is pure PyTorch: its "boundary" is the
+ * nn.Module API of src/codonlm/model_tiny_gpt.py and the op calls inside it.  Every
+ * entry point below replaces one such call site (cited per function), with plain
+ * pointers + sizes, no torch types.  All functions are stream-ordered on the
+ * caller's hipStream_t (passed as void*), never allocate, never synchronise, and
+ * return CG_OK (0) or a negative cg_status.  Buffers are caller-owned device memory.
+ *
+ * dtype codes: CG_F32 = fp32 storage/compute (parity mode), CG_BF16 = bf16 storage
+ * with fp32 accumulation (throughput mode).
+ */
+#ifndef CODONLM_HIP_H
+#define CODONLM_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { CG_F32 = 0, CG_BF16 = 1 };
+enum { CG_OK = 0, CG_EINVAL = -1, CG_EUNSUPPORTED = -2, CG_ELAUNCH = -3 };
+
+/* GEMM epilogue flags (bit set) */
+enum {
+  CG_EPI_BIAS = 1,       /* + bias[n] (fp32)                                           */
+  CG_EPI_GELU = 2,       /* out = gelu(v); aux_out (dtype of C) receives v (pre-act)   */
+  CG_EPI_DGELU = 4,      /* out = v * gelu'(aux[m,n]) (aux in dtype of C)              */
+  CG_EPI_RESID = 8,      /* out = resid[m,n] + v   (resid fp32, may alias C)           */
+  CG_EPI_DROPOUT = 16,   /* v = v * keep(seed, m, n) / (1-p) before RESID              */
+  CG_EPI_ACCUM = 32      /* out (fp32) += v                                            */
+};
+
+/*
+ * C[m,n] = epilogue( alpha * sum_k A(m,k) * B(n,k) )
+ *   A(m,k) = a_kcontig ? A[m*lda + k] : A[k*lda + m]
+ *   B(n,k) = b_kcontig ? B[n*ldb + k] : B[k*ldb + n]
+ * Replaces nn.Linear / matmul call sites of model_tiny_gpt.py:85-93,132,143-148,50-57,327
+ * and their autograd (dX = dY W, dW = dY^T X).  Inputs are `in_dtype`; C is c_dtype.
+ * Contiguous extents must be multiples of 8 and leading dims multiples of 8 elements.
+ * split_k > 1 needs `workspace` of split_k*M*N floats (dW GEMMs).
+ */
+typedef struct {
+  int in_dtype, c_dtype;
+  int M, N, K;
+  const void* A; long long lda; int a_kcontig;
+  const void* B; long long ldb; int b_kcontig;
+  void* C; long long ldc;
+  int epilogue;
+  float alpha;
+  const float* bias;
+  const float* resid; long long ldr;
+  const void* aux; void* aux_out; long long ld_aux;
+  uint32_t drop_seed; float drop_p;
+  int split_k; float* workspace;
+} cg_gemm_desc;
+int cg_gemm(const cg_gemm_desc* d, void* stream);
+
+/* LayerNorm (nn.LayerNorm, biased var, eps) -- model_tiny_gpt.py:137,139,216 */
+int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,
+                     const float* beta, void* y, long long ldy, float* mean, float* rstd,
+                     int rows, int cols, float eps, void* stream);
+/* dx = LN backward(dy) [+ g_in]; writes g_out (fp32) and optionally g_out_t (out_dtype,
+ * optionally multiplied by a dropout keep mask (seed,p) for the consumer branch);
+ * per-block column partials for dgamma/dbeta go to `partials` [nblk][2*cols]
+ * (nblk = cg_layernorm_bwd_blocks(rows)), reduced into dgamma/dbeta (accumulate flag). */
+int cg_layernorm_bwd_blocks(int rows);
+int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
+                     const float* mean, const float* rstd, const float* gamma,
+                     const float* g_in, float* g_out, int out_dtype, void* g_out_t,
+                     uint32_t drop_seed, float drop_p, float* partials, float* dgamma,
+                     float* dbeta, int accumulate, int rows, int cols, float eps, void* stream);
+
+/* token + position embedding (+dropout) -- model_tiny_gpt.py:305-312 */
+int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const float* pos_emb, float* x,
+                 int B, int T, int d, uint32_t drop_seed, float drop_p, void* stream);
+/* scatter-add backward into tok_emb grad (V rows) and pos grad; workspace size from
+ * cg_embed_bwd_workspace(B,T,V,d) */
+size_t cg_embed_bwd_workspace(int B, int T, int V, int d);
+int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, float* dpos, int B, int T,
+                 int V, int d, uint32_t drop_seed, float drop_p, int accumulate, void* ws,
+                 void* stream);
+
+/* segment starts from SEP ids: segstart[b,t] = last p<=t with idx[b,p]==sep (else 0);
+ * build_attention_mask's cumsum(idx==sep) equality, model_tiny_gpt.py:289-294 */
+int cg_segment_starts(const int64_t* idx, int32_t* segstart, int B, int T, int sep_id,
+                      void* stream);
+
+/* RoPE (half-split rotate_half) applied in place to the q and k column blocks of the
+ * packed qkv rows -- model_tiny_gpt.py:9-45,98-100.  cos_tab/sin_tab: fp32 [T][hd/2]
+ * built on the host exactly like RotaryEmbedding._set_cos_sin_cache.  inverse=1
+ * applies R^T (backward of the rotation). */
+int cg_rope_tab(int dtype, void* qkv, long long ldqkv, int B, int T, int H, int KV, int hd,
+                const float* cos_tab, const float* sin_tab, int inverse, void* stream);
+
+/* Fused causal + SEP-segment (+window) attention with GQA and attention-prob
+ * dropout, flash-style (no T x T materialisation) -- model_tiny_gpt.py:102-131.
+ * qkv rows: [q(H*hd) | k(KV*hd) | v(KV*hd)] with leading dim ldqkv; y: [B*T, H*hd];
+ * lse: [B*H*T] fp32 (natural-log logsumexp of the scaled scores). window<=0: none. */
+int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
+                void* y, long long ldy, float* lse, int B, int T, int H, int KV, int hd,
+                int window, uint32_t drop_seed, float drop_p, void* stream);
+/* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: cg_attn_bwd_workspace() */
+size_t cg_attn_bwd_workspace(int B, int T, int H);
+int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
+                const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
+                void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
+                uint32_t drop_seed, float drop_p, void* ws, void* stream);
+
+/* Label-smoothed, class-weighted, ignore_index cross-entropy fwd+bwd over logits rows
+ * (F.cross_entropy at model_tiny_gpt.py:343-349).  logits fp32 [rows][ldl], V used
+ * columns; writes loss (1 float, mean per the reference weighting), dlogits (dtype,
+ * pad columns [V,ldd) zeroed) scaled by `grad_scale`.  ws: cg_ce_workspace(rows) */
+size_t cg_ce_workspace(int rows);
+int cg_cross_entropy(const float* logits, long long ldl, const int64_t* targets, int rows,
+                     int V, float eps, const float* class_w, int ignore_index,
+                     float grad_scale, int d_dtype, void* dlogits, long long ldd,
+                     float* loss, void* ws, void* stream);
+
+/* SwiGLU: s = silu(gu[:, :H]) * gu[:, Hp:Hp+H] (model_tiny_gpt.py:57) and backward */
+int cg_swiglu_fwd(int dtype, const void* gu, long long ldgu, int Hp, void* s, long long lds,
+                  int rows, int H, void* stream);
+int cg_swiglu_bwd(int dtype, const void* gu, long long ldgu, int Hp, const void* ds,
+                  long long ldds, void* dgu, long long lddgu, int rows, int H, void* stream);
+
+/* column sums (bias gradients): out[n] (+)= sum_m X[m*ldx+n] */
+size_t cg_colsum_workspace(int rows, int cols);
+int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out,
+              int accumulate, void* ws, void* stream);
+
+/* elementwise casts / utilities */
+int cg_cast_f32_to_bf16(const float* src, uint16_t* dst, long long n, void* stream);
+int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stream);
+
+/* Fused AdamW over the flat parameter buffer (torch.optim.AdamW semantics,
+ * loop.py:681-731): up to 4 contiguous segments with their own (lr, wd); grads are
+ * multiplied by grad_scale (1/(n_micro*world)) first; optionally refreshes the bf16
+ * shadow copy used by the bf16 GEMMs.  step is the 1-based AdamW step count. */
+typedef struct { long long begin, end; float lr, wd; } cg_adamw_segment;
+int cg_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+             uint16_t* shadow_bf16, const cg_adamw_segment* segs, int nseg, float beta1,
+             float beta2, float eps, int step, float grad_scale, void* stream);
+/* nonfinite flag: flag |= any(!isfinite(x[0..n))) (device int) */
+int cg_nonfinite_flag(const float* x, long long n, int* flag, void* stream);
+
+/* ------------------------------------------------------------------------------
+ * Whole-model engine: the TinyGPT forward/backward sequence as one native call per
+ * phase (replaces TinyGPT.forward + loss.backward(), model_tiny_gpt.py:297-352,
+ * loop.py:1067-1233).  Parameters live in ONE flat fp32 buffer whose layout is owned
+ * by the library (cg_model_param_layout); grads use the same layout.
+ * ----------------------------------------------------------------------------*/
+typedef struct {
+  int vocab_size, block_size, n_layer, n_head, n_kv_head, n_embd;
+  int use_swiglu, use_rope, sep_id /* <0: none */, tie_embeddings;
+  int termination_aux, termination_n_classes;
+  int n_offsets; int offsets[8];
+  float dropout, label_smoothing, ln_eps;
+  int dtype; /* CG_F32 or CG_BF16 */
+} cg_model_cfg;
+
+/* parameter tensor kinds (layer = -1 for global tensors) */
+enum {
+  CG_P_TOK_EMB = 0, CG_P_POS_EMB, CG_P_LN1_W, CG_P_LN1_B, CG_P_Q_W, CG_P_K_W, CG_P_V_W,
+  CG_P_Q_B, CG_P_K_B, CG_P_V_B, CG_P_PROJ_W, CG_P_PROJ_B, CG_P_LN2_W, CG_P_LN2_B,
+  CG_P_FC1_W, CG_P_FC1_B, CG_P_FC2_W, CG_P_FC2_B, CG_P_GATE_W, CG_P_UP_W, CG_P_DOWN_W,
+  CG_P_LNF_W, CG_P_LNF_B, CG_P_HEAD_W, CG_P_TERM_W, CG_P_TERM_B, CG_P_OFF1_W, CG_P_OFF1_B,
+  CG_P_OFF2_W, CG_P_OFF2_B, CG_P_NKINDS
+};
+typedef struct {
+  int kind, layer;        /* layer: block index, offset index (OFF*), or -1 */
+  long long offset;       /* element offset into the flat buffer */
+  int rows, cols;         /* logical (state_dict) shape; cols=0 for 1-D */
+  long long ld;           /* row stride in elements (>= cols) */
+} cg_param_entry;
+/* returns number of entries (<= max) and the flat buffer size in *total_elems */
+int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* out, int max,
+                          long long* total_elems);
+size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T);
+
+typedef struct {
+  cg_model_cfg cfg;
+  float* params;            /* flat fp32 master */
+  const uint16_t* shadow;   /* flat bf16 copy (dtype==CG_BF16) */
+  float* grads;             /* flat fp32 grads, same layout */
+  const float* loss_weights;/* [V] or NULL (uniform) */
+  const float* rope_cos;    /* [block_size][hd/2] (use_rope) */
+  const float* rope_sin;
+  void* workspace; size_t workspace_bytes;
+  /* filled by cg_model_forward, consumed by cg_model_backward / cg_model_hidden */
+  int B, T, training, window;
+  uint32_t seed;
+  const int64_t* idx;
+  const int64_t* targets;
+  float* logits;
+} cg_model;
+
+/* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
+ * float; targets NULL => no loss).  With targets, d(loss)/d(logits) is produced here
+ * (fused CE fwd+bwd).  training enables dropout with `seed`; window<=0: no window. */
+int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, int B, int T,
+                     int training, uint32_t seed, int window, float* logits, float* loss,
+                     void* stream);
+/* backward in phases so the caller can overlap per-bucket gradient all-reduce:
+ *   phase 0: head + ln_f; phase 1: one block `layer` (call L-1 .. 0); phase 2: embeddings.
+ * accumulate=0 overwrites grads (first microbatch of a group), 1 adds. */
+int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* stream);
+/* pointer to hidden state `which` (0 = embedding output, 1..L = block outputs,
+ * L+1 = ln_f output) inside the workspace after a forward; dtype in *dtype_out */
+const void* cg_model_hidden(const cg_model* m, int which, int* dtype_out, long long* ld);
+
+const char* cg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,222 @@
+"""Op-level parity of the HIP kernels against plain PyTorch fp32 (CPU) references.
+
+Every test here needs the MI355X (marker ``gpu``) and calls through the C-ABI
+(libcodonlm_hip.so) via codonlm_amd.ops.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import tinygpt_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from codonlm_amd import ops
+    return ops
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).float()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("M,N,K", [(128, 64, 64), (200, 136, 72), (1024, 512, 384), (96, 80, 1000)])
+def test_gemm_layouts(dtype, ak, bk, M, N, K):
+    ops = _ops()
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    Am = torch.randn(M, K, generator=g)
+    Bn = torch.randn(N, K, generator=g)
+    a = (Am if ak else Am.t().contiguous()).to(DEV, dtype)
+    b = (Bn if bk else Bn.t().contiguous()).to(DEV, dtype)
+    out = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32)
+    ref = (_bf(Am) @ _bf(Bn).t()) if dtype == torch.bfloat16 else (Am.double() @ Bn.double().t()).float()
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    err = (out.cpu() - ref).abs().max().item()
+    assert err <= tol * max(1.0, math.sqrt(K)), err
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogues(dtype):
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    M, N, K = 256, 192, 128
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.1
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    xd, wd = x.to(DEV, dtype), w.to(DEV, dtype)
+    base = (_bf(x) @ _bf(w).t()) if dtype == torch.bfloat16 else x @ w.t()
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-4
+    # bias + gelu with pre-activation saved
+    aux = torch.empty(M, N, dtype=dtype, device=DEV)
+    y = ops.gemm(xd, wd, out_dtype=dtype, bias=bias.to(DEV), epilogue=L.EPI_BIAS | L.EPI_GELU, aux_out=aux)
+    pre = base + bias
+    assert (aux.float().cpu() - pre).abs().max() < tol * 4
+    assert (y.float().cpu() - F.gelu(pre)).abs().max() < tol * 4
+    # dgelu
+    y2 = ops.gemm(xd, wd, out_dtype=dtype, epilogue=L.EPI_DGELU, aux=aux)
+    xa = aux.float().cpu().requires_grad_(True)
+    F.gelu(xa).sum().backward()
+    ref2 = base * xa.grad
+    assert (y2.float().cpu() - ref2).abs().max() < tol * 4
+    # bias + dropout + residual (fp32 out)
+    p = 0.25
+    seed = 12345
+    y3 = ops.gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
+                  epilogue=L.EPI_BIAS | L.EPI_DROPOUT | L.EPI_RESID, drop_seed=seed, drop_p=p)
+    keep = torch.from_numpy(O.dropout_keep(seed, np.arange(M)[:, None], np.arange(N)[None, :], p))
+    ref3 = res + torch.where(keep, (base + bias) / (1 - p), torch.zeros(()))
+    assert (y3.cpu() - ref3).abs().max() < tol * 4
+    # accumulate + split-K
+    acc0 = torch.randn(M, N, generator=g)
+    out = acc0.clone().to(DEV)
+    ops.gemm(xd, wd, out=out, epilogue=L.EPI_ACCUM, split_k=3, alpha=0.5)
+    assert (out.cpu() - (acc0 + 0.5 * base)).abs().max() < tol * 4
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cols", [64, 384, 512, 100])
+def test_layernorm_fwd_bwd(out_dtype, cols):
+    ops = _ops()
+    rows = 300
+    g = torch.Generator().manual_seed(cols)
+    x = torch.randn(rows, cols, generator=g) * 3 + 1
+    w = 1 + 0.1 * torch.randn(cols, generator=g)
+    b = 0.1 * torch.randn(cols, generator=g)
+    y, mean, rstd = ops.layernorm_fwd(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype=out_dtype)
+    xr = x.clone().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    ref = F.layer_norm(xr, (cols,), wr, br, 1e-5)
+    tol = 2e-2 if out_dtype == torch.bfloat16 else 1e-5
+    assert (y.float().cpu() - ref.detach()).abs().max() < tol * 4
+    dy = torch.randn(rows, cols, generator=g)
+    gin = torch.randn(rows, cols, generator=g)
+    ref.backward(dy)
+    go, dgam, dbet = ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, w.to(DEV), g_in=gin.to(DEV))
+    assert (go.cpu() - (xr.grad + gin)).abs().max() < 1e-4
+    assert (dgam.cpu() - wr.grad).abs().max() < 1e-3
+    assert (dbet.cpu() - br.grad).abs().max() < 1e-3
+
+
+def test_segment_starts():
+    ops = _ops()
+    idx = torch.randint(4, 68, (3, 700))
+    idx[0, 5] = 3
+    idx[0, 300] = 3
+    idx[1, 0] = 3
+    idx[2, 699] = 3
+    got = ops.segment_starts(idx.to(DEV), 3).cpu()
+    exp = torch.zeros_like(got)
+    for b in range(3):
+        last = 0
+        for t in range(700):
+            if idx[b, t] == 3:
+                last = t
+            exp[b, t] = last
+    assert torch.equal(got, exp)
+
+
+def _attn_ref(qkv, idx, B, T, H, KV, hd, sep, window, drop=None):
+    q = qkv[:, : H * hd].view(B, T, H, hd).transpose(1, 2)
+    k = qkv[:, H * hd: (H + KV) * hd].view(B, T, KV, hd).transpose(1, 2)
+    v = qkv[:, (H + KV) * hd:].view(B, T, KV, hd).transpose(1, 2)
+    k = k.repeat_interleave(H // KV, 1)
+    v = v.repeat_interleave(H // KV, 1)
+    att = (q @ k.transpose(-2, -1)) / math.sqrt(hd)
+    m = O.attention_mask(idx, sep, window)
+    att = att.masked_fill(~m[:, None], float("-inf")).softmax(-1)
+    if drop is not None:
+        att = att * drop
+    return (att @ v).transpose(1, 2).reshape(B * T, H * hd)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,T,H,KV,hd,window,p", [
+    (2, 64, 4, 4, 16, 0, 0.0), (2, 200, 4, 2, 64, 0, 0.0), (1, 256, 8, 4, 48, 0, 0.0),
+    (2, 130, 2, 1, 32, 17, 0.0), (2, 96, 4, 4, 64, 0, 0.2)])
+def test_attention_fwd_bwd(dtype, B, T, H, KV, hd, window, p):
+    ops = _ops()
+    g = torch.Generator().manual_seed(T + H)
+    N = (H + 2 * KV) * hd
+    qkv = torch.randn(B * T, N, generator=g)
+    if dtype == torch.bfloat16:
+        qkv = _bf(qkv)
+    idx = torch.randint(4, 68, (B, T), generator=g)
+    idx[:, T // 3] = 3
+    idx[0, T // 2] = 3
+    seed = 777
+    drop = None
+    if p > 0:
+        keep = O.dropout_keep(seed, np.arange(B * H * T)[:, None], np.arange(T)[None, :], p)
+        drop = torch.from_numpy(keep.astype(np.float32) / (1 - p)).view(B, H, T, T)
+    qr = qkv.clone().requires_grad_(True)
+    ref = _attn_ref(qr, idx, B, T, H, KV, hd, 3, window or None, drop)
+    seg = ops.segment_starts(idx.to(DEV), 3)
+    qd = qkv.to(DEV, dtype)
+    y, lse = ops.attn_fwd(qd, seg, B, T, H, KV, hd, window=window, drop_seed=seed, drop_p=p)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert (y.float().cpu() - ref.detach()).abs().max() < tol
+    dy = torch.randn(B * T, H * hd, generator=g)
+    if dtype == torch.bfloat16:
+        dy = _bf(dy)
+    ref.backward(dy)
+    dq = ops.attn_bwd(qd, seg, y, dy.to(DEV, dtype), lse, B, T, H, KV, hd, window=window, drop_seed=seed, drop_p=p)
+    err = (dq.float().cpu() - qr.grad).abs().max().item()
+    scale = qr.grad.abs().max().item()
+    assert err < (5e-2 if dtype == torch.bfloat16 else 1e-4) * max(1.0, scale), err
+
+
+@pytest.mark.parametrize("eps,weighted", [(0.0, False), (0.05, False), (0.1, True)])
+def test_cross_entropy(eps, weighted):
+    ops = _ops()
+    rows, V = 517, 68
+    g = torch.Generator().manual_seed(11)
+    z = torch.randn(rows, V, generator=g) * 5
+    t = torch.randint(0, V, (rows,), generator=g)
+    t[:50] = 0
+    w = torch.rand(V, generator=g) + 0.5 if weighted else None
+    zr = z.clone().requires_grad_(True)
+    ref = F.cross_entropy(zr, t, ignore_index=0, label_smoothing=eps, weight=w)
+    ref.backward()
+    loss, dl = ops.cross_entropy(z.to(DEV), t.to(DEV), eps=eps, weight=w.to(DEV) if w is not None else None,
+                                 pad_to=80)
+    assert abs(loss.item() - ref.item()) < 1e-5 * max(1, abs(ref.item()))
+    assert (dl[:, :V].cpu() - zr.grad).abs().max() < 1e-6
+    assert torch.all(dl[:, V:] == 0)
+
+
+def test_cross_entropy_all_pad_is_nan():
+    ops = _ops()
+    z = torch.randn(8, 68, device=DEV)
+    t = torch.zeros(8, dtype=torch.long, device=DEV)
+    loss, _ = ops.cross_entropy(z, t)
+    assert math.isnan(loss.item())
+
+
+def test_adamw_matches_torch():
+    ops = _ops()
+    n = 10000
+    g = torch.Generator().manual_seed(5)
+    p0 = torch.randn(n, generator=g)
+    ps = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ps], lr=1e-3, weight_decay=0.05)
+    pd = p0.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    shadow = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    for step in range(1, 4):
+        grad = torch.randn(n, generator=g)
+        ps.grad = grad.clone()
+        opt.step()
+        ops.adamw_(pd, (grad * 4).to(DEV), m, v, step, [(0, n, 1e-3, 0.05)], shadow=shadow, grad_scale=0.25)
+    assert (pd.cpu() - ps.detach()).abs().max() < 1e-6
+    assert (shadow.float().cpu() - ps.detach()).abs().max() < 1e-2
