@@ -88,7 +88,9 @@ def test_c4_layer_grad_sums():
     loss.backward()
     for k, p in m.named_parameters():
         ref = g.get(f"gradsum/{k}")
-        if ref is None:
+        if ref is None or k.endswith("attn.key.bias"):
+            # softmax is shift-invariant per query row: d(loss)/d(key.bias) == 0 exactly,
+            # both sides hold only rounding noise (~1e-8)
             continue
         gg = p.grad.detach().double().cpu()
         tot, asum, sq = float(gg.sum()), float(gg.abs().sum()), float(gg.pow(2).sum())

@@ -1,0 +1,12 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=300 > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?
+echo "smoke rc=$rc" >> gpurun_out/smoke.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+true
+echo "bench rc=$?" >> gpurun_out/bench.log
