@@ -1,17 +1,584 @@
-// bf16 MFMA flash-attention kernels (gfx950).  Included by attention.hip.
+// bf16 MFMA flash attention for gfx950 (included by attention.hip).
+//
+// All products use v_mfma_f32_32x32x16_bf16.  Layout conventions (cdna_hip_programming §3):
+//   A frag: lane l holds A[row l&31][k = 8*(l>>5) + j], j = 0..7
+//   B frag: lane l holds B[k = 8*(l>>5) + j][col l&31]
+//   C/D   : lane l holds C[row (r&3) + 8*(r>>2) + 4*(l>>5)][col l&31], r = 0..15
+// "Swapped" products keep the query (or key) on the lane, so softmax statistics are
+// per-lane scalars; an accumulator whose rows are the reduction index of the next
+// product is fed to it as the B operand with no data movement (rows 8s..8s+7 of the
+// accumulator = k-step s, in the permuted k order k(j,h) = 16s + 8(j>>2) + 4h + (j&3)),
+// and the other operand is read from LDS with ds_read_b64_tr_b16 in that same order.
+//
+// Every K/V/Q/dO tile lives in LDS as a [64 rows][64 bf16] "dual" image whose 16-byte
+// chunks are XOR-swizzled so that both the row reads (ds_read_b128, 32 rows x 16 B) and
+// the transposed reads (ds_read_b64_tr_b16, 4 rows x 32 cols per half-wave) are
+// bank-conflict free (see dual_off).  Head dims < 64 are zero-padded in the image.
 #pragma once
 
-static inline bool attn_mfma_supported(int hd, long long ld_in, long long ld_out) {
-  (void)hd; (void)ld_in; (void)ld_out;
-  return false;  // enabled once the MFMA kernels land
+namespace fa {
+constexpr int HDP = 64;        // padded head dim held in LDS / registers
+constexpr int KT = 64;         // rows per staged tile
+constexpr int IMG = KT * 128;  // bytes of one [64][64] bf16 image
+
+__device__ __forceinline__ int dual_off(int row, int ch) {
+  const int j = row >> 1;
+  const int g = (j & 7) ^ ((j & 1) << 2);
+  return row * 128 + 16 * (ch ^ g);
 }
 
-static inline int attn_fwd_mfma_launch(const bf16_t*, long long, const int32_t*, bf16_t*, long long, float*, int, int,
-                                       int, int, int, int, uint32_t, uint32_t, float, float, hipStream_t) {
-  return CG_EUNSUPPORTED;
+struct Stage2 { uint4 v[2]; };
+
+// 64 rows x 8 chunks (16 B) = 512 chunks, 256 threads -> 2 each.  Rows >= rlim and
+// columns >= hd are zero-filled.
+__device__ __forceinline__ void tile_load(Stage2& s, const bf16_t* base, long long ld, int r0, int rlim, int hd,
+                                          int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i, row = c >> 3, ch = c & 7;
+    if (r0 + row < rlim && ch * 8 < hd) s.v[i] = *(const uint4*)(base + (long long)(r0 + row) * ld + ch * 8);
+    else s.v[i] = make_uint4(0, 0, 0, 0);
+  }
 }
-static inline int attn_bwd_mfma_launch(const bf16_t*, long long, const int32_t*, const bf16_t*, long long,
-                                       const float*, const float*, bf16_t*, long long, int, int, int, int, int, int,
-                                       uint32_t, uint32_t, float, float, hipStream_t) {
-  return CG_EUNSUPPORTED;
+__device__ __forceinline__ void tile_store(const Stage2& s, char* img, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i;
+    *(uint4*)(img + dual_off(c >> 3, c & 7)) = s.v[i];
+  }
+}
+
+// A operand, rows rb..rb+31 of the image on the lane, k-step ks (16 columns)
+__device__ __forceinline__ v8bf frag_row(const char* img, int rb, int ks, int lane) {
+  return *(const v8bf*)(img + dual_off(rb + (lane & 31), 2 * ks + (lane >> 5)));
+}
+
+typedef v4s __attribute__((address_space(3))) * lds_v4s_p;
+
+// A operand = transpose of the image: A[m = column cb*32 + (l&31)][k = image rows in the
+// accumulator-permuted order of k-step s within the 32-row block rb]
+__device__ __forceinline__ v8bf frag_tr(const char* img, int rb, int s, int cb, int lane) {
+  const int h = lane >> 5, g16 = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  const int ch = ((cb * 32 + g16 * 16) >> 3) + (p >> 1);
+  const int ra = rb + 16 * s + 4 * h + q;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + dual_off(ra, ch) + 8 * (p & 1)));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + dual_off(ra + 8, ch) + 8 * (p & 1)));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
+
+// B operand from an accumulator: rows 8s..8s+7 as bf16
+__device__ __forceinline__ v8bf pack_b(const v16f& x, int s) {
+  v8bf r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)x[8 * s + j];
+  return r;
+}
+
+// B operand straight from global: row `row` (the lane's column index), k-step ks
+__device__ __forceinline__ v8bf frag_global(const bf16_t* rowp, bool ok, int ks, int hd, int lane) {
+  const int c = ks * 16 + 8 * (lane >> 5);
+  if (ok && c < hd) return *(const v8bf*)(rowp + c);
+  v8bf z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = (__bf16)0.f;
+  return z;
+}
+
+__device__ __forceinline__ v16f zero16() {
+  v16f z;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z[i] = 0.f;
+  return z;
+}
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+// visible-key lower bound for query q (monotone non-decreasing in q)
+__device__ __forceinline__ int lo_of(const int32_t* seg, long long rowbase, int q, int T, int window) {
+  if (q >= T) q = T - 1;
+  int lo = seg ? seg[rowbase + q] : 0;
+  if (window > 0) lo = max(lo, q - window + 1);
+  return lo;
+}
+}  // namespace fa
+
+// ============================================================================
+// forward: WG = 4 waves x 32 queries (128), key tiles of 64, K/V double-buffered
+// ============================================================================
+__global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, long long ld,
+                                                        const int32_t* __restrict__ seg, bf16_t* __restrict__ y,
+                                                        long long ldy, float* __restrict__ lse, int T, int H, int KV,
+                                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale,
+                                                        float scale) {
+  using namespace fa;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
+  const int bh = blockIdx.y, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
+  const int qtile = gridDim.x - 1 - blockIdx.x;  // heaviest (latest) query tiles first
+  const int q0 = qtile * 128, q0w = q0 + wave * 32;
+  const int myq = q0w + (lane & 31);
+  const bool qok = myq < T;
+  const long long rowbase = (long long)b * T;
+  const bf16_t* qrow = qkv + (rowbase + (qok ? myq : 0)) * ld + (long long)hh * hd;
+  v8bf qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = frag_global(qrow, qok, ks, hd, lane);
+  const int lo = qok ? lo_of(seg, rowbase, myq, T, window) : 0x7fffffff;
+  const int kmin = lo_of(seg, rowbase, q0, T, window);
+  const int kmax = min(T - 1, q0 + 127);
+  const int w_lo_min = lo_of(seg, rowbase, q0w, T, window);
+  const int w_lo_max = lo_of(seg, rowbase, min(q0w + 31, T - 1), T, window);
+  const int w_qmax = min(T - 1, q0w + 31);
+  const bf16_t* kbase = qkv + rowbase * ld + (long long)H * hd + (long long)kvh * hd;
+  const bf16_t* vbase = qkv + rowbase * ld + (long long)(H + KV) * hd + (long long)kvh * hd;
+  const float c = scale * 1.4426950408889634f;
+  const uint32_t drow = (uint32_t)(((long long)b * H + hh) * T + myq);
+  const int nks = (hd + 15) >> 4;
+
+  float m = -INFINITY, lsum = 0.f;
+  v16f o0 = zero16(), o1 = zero16();
+  const int t0 = kmin / KT, t1 = kmax / KT;
+  Stage2 sk, sv;
+  tile_load(sk, kbase, ld, t0 * KT, T, hd, tid);
+  tile_load(sv, vbase, ld, t0 * KT, T, hd, tid);
+  tile_store(sk, smem, tid);
+  tile_store(sv, smem + IMG, tid);
+  __syncthreads();
+  for (int t = t0; t <= t1; ++t) {
+    const int cur = (t - t0) & 1;
+    const char* Ki = smem + cur * 2 * IMG;
+    const char* Vi = Ki + IMG;
+    const bool more = t < t1;
+    if (more) {
+      tile_load(sk, kbase, ld, (t + 1) * KT, T, hd, tid);
+      tile_load(sv, vbase, ld, (t + 1) * KT, T, hd, tid);
+    }
+    const int k0 = t * KT;
+    if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
+      v16f s0 = zero16(), s1 = zero16();
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks < nks) {
+          s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 0, ks, lane), qf[ks], s0, 0, 0, 0);
+          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 32, ks, lane), qf[ks], s1, 0, 0, 0);
+        }
+      }
+      const bool full = (k0 + KT - 1 <= q0w) && (k0 >= w_lo_max);
+      if (!full) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key0 = k0 + acc_row(r, lane), key1 = key0 + 32;
+          if (key0 > myq || key0 < lo) s0[r] = -INFINITY;
+          if (key1 > myq || key1 < lo) s1[r] = -INFINITY;
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float mu = (mn == -INFINITY) ? 0.f : mn;
+      const float alpha = exp2f((m - mu) * c);
+      const float mc = mu * c;
+      lsum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+      float ps = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = exp2f(fmaf(s0[r], c, -mc));
+        s1[r] = exp2f(fmaf(s1[r], c, -mc));
+        ps += s0[r] + s1[r];
+      }
+      lsum += ps;
+      if (thr) {
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int key0 = k0 + acc_row(r, lane);
+          const uint32_t h0 = cg_hash_pair(seed, drow, (uint32_t)key0 >> 1);
+          const uint32_t h1 = cg_hash_pair(seed, drow, (uint32_t)(key0 + 32) >> 1);
+          s0[r] = (h0 & 0xFFFFu) >= thr ? s0[r] * dscale : 0.f;
+          s0[r + 1] = (h0 >> 16) >= thr ? s0[r + 1] * dscale : 0.f;
+          s1[r] = (h1 & 0xFFFFu) >= thr ? s1[r] * dscale : 0.f;
+          s1[r + 1] = (h1 >> 16) >= thr ? s1[r + 1] * dscale : 0.f;
+        }
+      }
+      const v8bf p00 = pack_b(s0, 0), p01 = pack_b(s0, 1), p10 = pack_b(s1, 0), p11 = pack_b(s1, 1);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 0, lane), p00, o0, 0, 0, 0);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 0, lane), p01, o0, 0, 0, 0);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 0, lane), p10, o0, 0, 0, 0);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 0, lane), p11, o0, 0, 0, 0);
+      if (hd > 32) {
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 1, lane), p00, o1, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 1, lane), p01, o1, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 1, lane), p10, o1, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 1, lane), p11, o1, 0, 0, 0);
+      }
+      m = mn;
+    }
+    if (more) {
+      char* nk = smem + (cur ^ 1) * 2 * IMG;
+      tile_store(sk, nk, tid);
+      tile_store(sv, nk + IMG, tid);
+    }
+    __syncthreads();
+  }
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  if (qok) {
+    const float inv = 1.0f / ltot;
+    bf16_t* yr = y + (rowbase + myq) * ldy + (long long)hh * hd;
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) {
+      const int d0 = acc_row(r, lane);
+      if (d0 < hd) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(o0[r] * inv) | ((uint32_t)f2bf(o0[r + 1] * inv) << 16);
+        w.y = (uint32_t)f2bf(o0[r + 2] * inv) | ((uint32_t)f2bf(o0[r + 3] * inv) << 16);
+        *(uint2*)(yr + d0) = w;
+      }
+      if (d0 + 32 < hd) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(o1[r] * inv) | ((uint32_t)f2bf(o1[r + 1] * inv) << 16);
+        w.y = (uint32_t)f2bf(o1[r + 2] * inv) | ((uint32_t)f2bf(o1[r + 3] * inv) << 16);
+        *(uint2*)(yr + d0 + 32) = w;
+      }
+    }
+    if (hl == 0) lse[((long long)b * H + hh) * T + myq] = m * scale + __logf(ltot);
+  }
+}
+
+// ============================================================================
+// backward dQ: WG = 4 waves x 32 queries; key tiles of 64 (K, V images)
+// dS^T = P^T o (dP^T - delta),  dQ^T[d][q] += K^T[d][key] dS^T[key][q]
+// ============================================================================
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, long long ld,
+                                                           const int32_t* __restrict__ seg,
+                                                           const bf16_t* __restrict__ dy, long long lddy,
+                                                           const float* __restrict__ lse,
+                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                           long long lddq, int T, int H, int KV, int hd, int window,
+                                                           uint32_t seed, uint32_t thr, float dscale, float scale) {
+  using namespace fa;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int bh = blockIdx.y, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
+  const int qtile = gridDim.x - 1 - blockIdx.x;
+  const int q0 = qtile * 128, q0w = q0 + wave * 32;
+  const int myq = q0w + (lane & 31);
+  const bool qok = myq < T;
+  const long long rowbase = (long long)b * T;
+  const bf16_t* qrow = qkv + (rowbase + (qok ? myq : 0)) * ld + (long long)hh * hd;
+  const bf16_t* dorow = dy + (rowbase + (qok ? myq : 0)) * lddy + (long long)hh * hd;
+  v8bf qf[4], df[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    qf[ks] = frag_global(qrow, qok, ks, hd, lane);
+    df[ks] = frag_global(dorow, qok, ks, hd, lane);
+  }
+  const long long bhq = ((long long)b * H + hh) * T + (qok ? myq : 0);
+  const float c = scale * 1.4426950408889634f;
+  const float lse2 = qok ? lse[bhq] * 1.4426950408889634f : 0.f;
+  const float dl = qok ? delta[bhq] : 0.f;
+  const int lo = qok ? lo_of(seg, rowbase, myq, T, window) : 0x7fffffff;
+  const int kmin = lo_of(seg, rowbase, q0, T, window);
+  const int kmax = min(T - 1, q0 + 127);
+  const int w_lo_min = lo_of(seg, rowbase, q0w, T, window);
+  const int w_lo_max = lo_of(seg, rowbase, min(q0w + 31, T - 1), T, window);
+  const int w_qmax = min(T - 1, q0w + 31);
+  const bf16_t* kbase = qkv + rowbase * ld + (long long)H * hd + (long long)kvh * hd;
+  const bf16_t* vbase = qkv + rowbase * ld + (long long)(H + KV) * hd + (long long)kvh * hd;
+  const uint32_t drow = (uint32_t)bhq;
+  const int nks = (hd + 15) >> 4;
+  v16f a0 = zero16(), a1 = zero16();
+  const int t0 = kmin / KT, t1 = kmax / KT;
+  Stage2 sk, sv;
+  tile_load(sk, kbase, ld, t0 * KT, T, hd, tid);
+  tile_load(sv, vbase, ld, t0 * KT, T, hd, tid);
+  tile_store(sk, smem, tid);
+  tile_store(sv, smem + IMG, tid);
+  __syncthreads();
+  for (int t = t0; t <= t1; ++t) {
+    const int cur = (t - t0) & 1;
+    const char* Ki = smem + cur * 2 * IMG;
+    const char* Vi = Ki + IMG;
+    const bool more = t < t1;
+    if (more) {
+      tile_load(sk, kbase, ld, (t + 1) * KT, T, hd, tid);
+      tile_load(sv, vbase, ld, (t + 1) * KT, T, hd, tid);
+    }
+    const int k0 = t * KT;
+    if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
+      const bool full = (k0 + KT - 1 <= q0w) && (k0 >= w_lo_max);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        v16f s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          if (ks < nks) {
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, kb * 32, ks, lane), qf[ks], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Vi, kb * 32, ks, lane), df[ks], dp, 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const int key = k0 + kb * 32 + acc_row(r, lane);
+          float p0 = exp2f(fmaf(s[r], c, -lse2)), p1 = exp2f(fmaf(s[r + 1], c, -lse2));
+          if (!full) {
+            if (key > myq || key < lo) p0 = 0.f;
+            if (key + 1 > myq || key + 1 < lo) p1 = 0.f;
+          }
+          float d0 = dp[r], d1 = dp[r + 1];
+          if (thr) {
+            const uint32_t hsh = cg_hash_pair(seed, drow, (uint32_t)key >> 1);
+            d0 = (hsh & 0xFFFFu) >= thr ? d0 * dscale : 0.f;
+            d1 = (hsh >> 16) >= thr ? d1 * dscale : 0.f;
+          }
+          s[r] = p0 * (d0 - dl);
+          s[r + 1] = p1 * (d1 - dl);
+        }
+        const v8bf b0 = pack_b(s, 0), b1 = pack_b(s, 1);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 0, 0, lane), b0, a0, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 1, 0, lane), b1, a0, 0, 0, 0);
+        if (hd > 32) {
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 0, 1, lane), b0, a1, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 1, 1, lane), b1, a1, 0, 0, 0);
+        }
+      }
+    }
+    if (more) {
+      char* nk = smem + (cur ^ 1) * 2 * IMG;
+      tile_store(sk, nk, tid);
+      tile_store(sv, nk + IMG, tid);
+    }
+    __syncthreads();
+  }
+  if (qok) {
+    bf16_t* dr = dqkv + (rowbase + myq) * lddq + (long long)hh * hd;
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) {
+      const int d0 = acc_row(r, lane);
+      if (d0 < hd) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(a0[r] * scale) | ((uint32_t)f2bf(a0[r + 1] * scale) << 16);
+        w.y = (uint32_t)f2bf(a0[r + 2] * scale) | ((uint32_t)f2bf(a0[r + 3] * scale) << 16);
+        *(uint2*)(dr + d0) = w;
+      }
+      if (d0 + 32 < hd) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(a1[r] * scale) | ((uint32_t)f2bf(a1[r + 1] * scale) << 16);
+        w.y = (uint32_t)f2bf(a1[r + 2] * scale) | ((uint32_t)f2bf(a1[r + 3] * scale) << 16);
+        *(uint2*)(dr + d0 + 32) = w;
+      }
+    }
+  }
+}
+
+// ============================================================================
+// backward dK/dV: WG = 4 waves x 32 keys (128 keys of one (b, kv head)); loops over
+// the group's query heads and query tiles of 64 (Q, dO images + lse/delta/lo rows).
+//   S = Q K^T, dP = dO V^T (query rows in registers, key on the lane)
+//   dV^T[d][key] += dO^T[d][q] Pd[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
+// ============================================================================
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv, long long ld,
+                                                             const int32_t* __restrict__ seg,
+                                                             const bf16_t* __restrict__ dy, long long lddy,
+                                                             const float* __restrict__ lse,
+                                                             const float* __restrict__ delta,
+                                                             bf16_t* __restrict__ dqkv, long long lddq, int T, int H,
+                                                             int KV, int hd, int window, uint32_t seed, uint32_t thr,
+                                                             float dscale, float scale) {
+  using namespace fa;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  // per buffer: Q image | dO image | lse2[64] | delta[64] | lo[64]
+  constexpr int BUF = 2 * IMG + 3 * 64 * 4;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int bk = blockIdx.y, b = bk / KV, kvh = bk % KV;
+  const int rep = H / KV;
+  const int ktile = gridDim.x - 1 - blockIdx.x;  // early keys see the most queries: first
+  const int kt0 = ktile * 128, kw0 = kt0 + wave * 32;
+  const int mykey = kw0 + (lane & 31);
+  const bool kok = mykey < T;
+  const long long rowbase = (long long)b * T;
+  const long long koff = (long long)H * hd + (long long)kvh * hd;
+  const long long voff = (long long)(H + KV) * hd + (long long)kvh * hd;
+  const bf16_t* krow = qkv + (rowbase + (kok ? mykey : 0)) * ld + koff;
+  const bf16_t* vrow = qkv + (rowbase + (kok ? mykey : 0)) * ld + voff;
+  v8bf kf[4], vf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    kf[ks] = frag_global(krow, kok, ks, hd, lane);
+    vf[ks] = frag_global(vrow, kok, ks, hd, lane);
+  }
+  const float c = scale * 1.4426950408889634f;
+  const int nks = (hd + 15) >> 4;
+  v16f dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
+  // query tile range: causal start; stop once every query's segment/window starts after the tile
+  const int qt_begin = kt0 / KT;
+  int qend = T;
+  if (window > 0) qend = min(T, kt0 + 127 + window);
+  const int qt_end = (qend - 1) / KT;  // inclusive
+  const int nqt = qt_end - qt_begin + 1;
+  const int total = nqt * rep;
+  auto stage_load = [&](Stage2& sq, Stage2& sd, int it) {
+    const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
+    tile_load(sq, qkv + rowbase * ld + (long long)h2 * hd, ld, qt * KT, T, hd, tid);
+    tile_load(sd, dy + rowbase * lddy + (long long)h2 * hd, lddy, qt * KT, T, hd, tid);
+  };
+  auto stage_store = [&](const Stage2& sq, const Stage2& sd, int it, char* buf) {
+    tile_store(sq, buf, tid);
+    tile_store(sd, buf + IMG, tid);
+    if (tid < 64) {
+      const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
+      const int q = qt * KT + tid;
+      const long long bhq = ((long long)b * H + h2) * T + (q < T ? q : 0);
+      float* fl = (float*)(buf + 2 * IMG);
+      int* il = (int*)(buf + 2 * IMG + 2 * 64 * 4);
+      fl[tid] = q < T ? lse[bhq] * 1.4426950408889634f : 0.f;
+      fl[64 + tid] = q < T ? delta[bhq] : 0.f;
+      il[tid] = q < T ? lo_of(seg, rowbase, q, T, window) : 0x7fffffff;
+    }
+  };
+  Stage2 sq, sd;
+  if (total > 0) {
+    stage_load(sq, sd, 0);
+    stage_store(sq, sd, 0, smem);
+  }
+  __syncthreads();
+  for (int it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    const char* buf = smem + cur * BUF;
+    const char* Qi = buf;
+    const char* Di = buf + IMG;
+    const float* lse2s = (const float*)(buf + 2 * IMG);
+    const float* dls = lse2s + 64;
+    const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
+    const bool more = it + 1 < total;
+    if (more) stage_load(sq, sd, it + 1);
+    const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
+    const int q0 = qt * KT;
+    const uint32_t drow0 = (uint32_t)(((long long)b * H + h2) * T);
+    // wave activity: some query q in [q0, q0+63] sees some key in [kw0, kw0+31]
+    const int qlast = min(T - 1, q0 + KT - 1);
+    const bool active = (qlast >= kw0) && (los[0] <= kw0 + 31);
+    if (active) {
+      const bool full = (q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (los[qlast - q0] <= kw0);
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        v16f s = zero16(), dp = zero16();
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          if (ks < nks) {
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Qi, qb * 32, ks, lane), kf[ks], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Di, qb * 32, ks, lane), vf[ks], dp, 0, 0, 0);
+          }
+        }
+        v16f pd;
+#pragma unroll
+        for (int rg = 0; rg < 16; rg += 4) {
+          const int qi = qb * 32 + acc_row(rg, lane);  // 4 consecutive queries qi..qi+3
+          const float4 l4 = *(const float4*)(lse2s + qi);
+          const float4 d4 = *(const float4*)(dls + qi);
+          const int4 lo4 = *(const int4*)(los + qi);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+          const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+          const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = rg + u;
+            const int q = q0 + qi + u;
+            float p = exp2f(fmaf(s[r], c, -lv[u]));
+            if (!full && (mykey > q || mykey < lov[u] || q >= T)) p = 0.f;
+            float d = dp[r];
+            float pdr = p;
+            if (thr) {
+              const uint32_t hsh = cg_hash_pair(seed, drow0 + (uint32_t)q, (uint32_t)mykey >> 1);
+              const uint32_t bits = (mykey & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
+              const bool keep = bits >= thr;
+              d = keep ? d * dscale : 0.f;
+              pdr = keep ? p * dscale : 0.f;
+            }
+            pd[r] = pdr;
+            s[r] = p * (d - dv4[u]);
+          }
+        }
+        const v8bf pb0 = pack_b(pd, 0), pb1 = pack_b(pd, 1);
+        const v8bf sb0 = pack_b(s, 0), sb1 = pack_b(s, 1);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 0, 0, lane), pb0, dv0, 0, 0, 0);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 1, 0, lane), pb1, dv0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 0, 0, lane), sb0, dk0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 1, 0, lane), sb1, dk0, 0, 0, 0);
+        if (hd > 32) {
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 0, 1, lane), pb0, dv1, 0, 0, 0);
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 1, 1, lane), pb1, dv1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 0, 1, lane), sb0, dk1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 1, 1, lane), sb1, dk1, 0, 0, 0);
+        }
+      }
+    }
+    if (more) stage_store(sq, sd, it + 1, smem + (cur ^ 1) * BUF);
+    __syncthreads();
+  }
+  if (kok) {
+    bf16_t* kr = dqkv + (rowbase + mykey) * lddq + koff;
+    bf16_t* vr = dqkv + (rowbase + mykey) * lddq + voff;
+#pragma unroll
+    for (int r = 0; r < 16; r += 4) {
+      const int d0 = acc_row(r, lane);
+      if (d0 < hd) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(dk0[r] * scale) | ((uint32_t)f2bf(dk0[r + 1] * scale) << 16);
+        w.y = (uint32_t)f2bf(dk0[r + 2] * scale) | ((uint32_t)f2bf(dk0[r + 3] * scale) << 16);
+        *(uint2*)(kr + d0) = w;
+        w.x = (uint32_t)f2bf(dv0[r]) | ((uint32_t)f2bf(dv0[r + 1]) << 16);
+        w.y = (uint32_t)f2bf(dv0[r + 2]) | ((uint32_t)f2bf(dv0[r + 3]) << 16);
+        *(uint2*)(vr + d0) = w;
+      }
+      if (d0 + 32 < hd) {
+        uint2 w;
+        w.x = (uint32_t)f2bf(dk1[r] * scale) | ((uint32_t)f2bf(dk1[r + 1] * scale) << 16);
+        w.y = (uint32_t)f2bf(dk1[r + 2] * scale) | ((uint32_t)f2bf(dk1[r + 3] * scale) << 16);
+        *(uint2*)(kr + d0 + 32) = w;
+        w.x = (uint32_t)f2bf(dv1[r]) | ((uint32_t)f2bf(dv1[r + 1]) << 16);
+        w.y = (uint32_t)f2bf(dv1[r + 2]) | ((uint32_t)f2bf(dv1[r + 3]) << 16);
+        *(uint2*)(vr + d0 + 32) = w;
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+static inline bool attn_mfma_supported(int hd, long long ld_in, long long ld_out) {
+  if (getenv("CG_ATTN_VEC")) return false;  // diagnostic: force the vector kernels
+  return (hd == 32 || hd == 48 || hd == 64) && (ld_in % 8 == 0) && (ld_out % 8 == 0);
+}
+
+static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, bf16_t* y, long long ldy,
+                                       float* lse, int B, int T, int H, int KV, int hd, int window, uint32_t seed,
+                                       uint32_t thr, float dscale, float scale, hipStream_t s) {
+  dim3 g(cg_cdiv(T, 128), B * H);
+  const size_t sh = 4 * fa::IMG;
+  hipLaunchKernelGGL(attn_fwd_mfma, g, dim3(256), sh, s, qkv, ld, seg, y, ldy, lse, T, H, KV, hd, window, seed, thr,
+                     dscale, scale);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, const bf16_t* dy,
+                                       long long lddy, const float* lse, const float* delta, bf16_t* dqkv,
+                                       long long lddq, int B, int T, int H, int KV, int hd, int window,
+                                       uint32_t seed, uint32_t thr, float dscale, float scale, hipStream_t s) {
+  dim3 gq(cg_cdiv(T, 128), B * H);
+  hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv,
+                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale);
+  CG_LAUNCH_CHECK();
+  dim3 gk(cg_cdiv(T, 128), B * KV);
+  const size_t shk = 2 * (2 * fa::IMG + 3 * 64 * 4);
+  hipLaunchKernelGGL(attn_bwd_dkdv_mfma, gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv, lddq, T,
+                     H, KV, hd, window, seed, thr, dscale, scale);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
 }
