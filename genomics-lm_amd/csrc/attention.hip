@@ -305,6 +305,12 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
   const float scale = 1.0f / sqrtf((float)hd);
   float* delta = (float*)ws;
   const long long nbt = (long long)B * H * T;
+  if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, lddy) && (lddqkv & 7) == 0 && (ldy & 7) == 0) {
+    // delta = rowsum(dO o O) is computed inside the dQ kernel
+    return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)y, ldy, (const bf16_t*)dy,
+                                lddy, lse, delta, (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr,
+                                dscale, scale, s);
+  }
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const bf16_t*)y, ldy,
                        (const bf16_t*)dy, lddy, delta, B, T, H, hd);
@@ -313,10 +319,6 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
                        (const float*)dy, lddy, delta, B, T, H, hd);
   }
   CG_LAUNCH_CHECK();
-  if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, lddy) && (lddqkv & 7) == 0) {
-    return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)dy, lddy, lse, delta,
-                                (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr, dscale, scale, s);
-  }
   dim3 gq(cg_cdiv(T, AV_TQ), B * H), gk(cg_cdiv(T, AV_TQ), B * KV);
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_bwd_dq_vec<bf16_t>, gq, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart,

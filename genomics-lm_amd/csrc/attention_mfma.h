@@ -258,8 +258,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, long long ld,
                                                            const int32_t* __restrict__ seg,
                                                            const bf16_t* __restrict__ dy, long long lddy,
+                                                           const bf16_t* __restrict__ yo, long long ldy,
                                                            const float* __restrict__ lse,
-                                                           const float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                           float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                            long long lddq, int T, int H, int KV, int hd, int window,
                                                            uint32_t seed, uint32_t thr, float dscale, float scale) {
   using namespace fa;
@@ -273,16 +274,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
   const long long rowbase = (long long)b * T;
   const bf16_t* qrow = qkv + (rowbase + (qok ? myq : 0)) * ld + (long long)hh * hd;
   const bf16_t* dorow = dy + (rowbase + (qok ? myq : 0)) * lddy + (long long)hh * hd;
+  const bf16_t* orow = yo + (rowbase + (qok ? myq : 0)) * ldy + (long long)hh * hd;
   v8bf qf[4], df[4];
+  float dpart = 0.f;  // delta = rowsum(dO o O), the FA2 preprocessing, fused here
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     qf[ks] = frag_global(qrow, qok, ks, hd, lane);
     df[ks] = frag_global(dorow, qok, ks, hd, lane);
+    const v8bf of = frag_global(orow, qok, ks, hd, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dpart += (float)df[ks][j] * (float)of[j];
   }
   const long long bhq = ((long long)b * H + hh) * T + (qok ? myq : 0);
   const float c = scale * 1.4426950408889634f;
   const float lse2 = qok ? lse[bhq] * 1.4426950408889634f : 0.f;
-  const float dl = qok ? delta[bhq] : 0.f;
+  const float dl = dpart + __shfl_xor(dpart, 32, 64);
+  if (qok && lane < 32) delta[bhq] = dl;
   const int lo = qok ? lo_of(seg, rowbase, myq, T, window) : 0x7fffffff;
   const int kmin = lo_of(seg, rowbase, q0, T, window);
   const int kmax = min(T - 1, q0 + 127);
@@ -567,13 +574,14 @@ static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   return CG_OK;
 }
 
-static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, const bf16_t* dy,
-                                       long long lddy, const float* lse, const float* delta, bf16_t* dqkv,
-                                       long long lddq, int B, int T, int H, int KV, int hd, int window,
-                                       uint32_t seed, uint32_t thr, float dscale, float scale, hipStream_t s) {
+static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, const bf16_t* y,
+                                       long long ldy, const bf16_t* dy, long long lddy, const float* lse,
+                                       float* delta, bf16_t* dqkv, long long lddq, int B, int T, int H, int KV,
+                                       int hd, int window, uint32_t seed, uint32_t thr, float dscale, float scale,
+                                       hipStream_t s) {
   dim3 gq(cg_cdiv(T, 128), B * H);
-  hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv,
-                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale);
+  hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse, delta,
+                     dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);
   CG_LAUNCH_CHECK();
   dim3 gk(cg_cdiv(T, 128), B * KV);
   const size_t shk = 2 * (2 * fa::IMG + 3 * 64 * 4);

@@ -189,7 +189,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.g = w.take<float>(M * d * 4);
   A.dtmp = w.take<float>(M * d * 4);
   A.delta = w.take<float>((size_t)B * D.H * T * 4);
-  A.lnpart = w.take<float>((size_t)256 * 2 * d * 4);
+  A.lnpart = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 2 * d * 4);
   const long long maxcols = std::max<long long>({big, (long long)d, (long long)D.Hp});
   A.colws = w.take<float>((size_t)64 * maxcols * 4);
   long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,

@@ -221,11 +221,117 @@ __device__ __forceinline__ v8bf frag(const char* img, int rr0, int ks, int lane)
 }
 }  // namespace bfg
 
-template <bool AK, bool BKC>
-__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmParams p) {
+// ---------------------------------------------------------------------------
+// Vectorised epilogue: 8 consecutive columns of one row (N % 8 == 0 on this path).
+// EPI >= 0: compile-time epilogue flags / C dtype; EPI == -1: read them from p.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void ld8f(const float* p, float v[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(float* p, const float v[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ void ld8b(const bf16_t* p, float v[8]) {
+  const uint4 u = *(const uint4*)p;
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+}
+__device__ __forceinline__ void st8b(bf16_t* p, const float v[8]) {
+  uint4 u;
+  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  *(uint4*)p = u;
+}
+
+template <int EPI, int CT>
+__device__ __forceinline__ void epi_apply8(const GemmParams& p, int row, int col, float v[8]) {
+  const int e = EPI >= 0 ? EPI : p.epi;
+  const int ct = EPI >= 0 ? CT : p.c_dtype;
+  if (e & CG_EPI_BIAS) {
+    float bb[8];
+    ld8f(p.bias + col, bb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += bb[j];
+  }
+  const long long ai = (long long)row * p.ld_aux + col;
+  if (e & CG_EPI_GELU) {
+    if (ct == CG_BF16) st8b((bf16_t*)p.aux_out + ai, v);
+    else st8f((float*)p.aux_out + ai, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+  }
+  if (e & CG_EPI_DGELU) {
+    float a[8];
+    if (ct == CG_BF16) ld8b((const bf16_t*)p.aux + ai, a);
+    else ld8f((const float*)p.aux + ai, a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= dgelu_f(a[j]);
+  }
+  if (e & CG_EPI_DROPOUT) {
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const uint32_t h = cg_hash_pair(p.drop_seed, (uint32_t)row, (uint32_t)(col + j) >> 1);
+      v[j] = (h & 0xFFFFu) >= p.drop_thr ? v[j] * p.drop_scale : 0.f;
+      v[j + 1] = (h >> 16) >= p.drop_thr ? v[j + 1] * p.drop_scale : 0.f;
+    }
+  }
+  if (e & CG_EPI_RESID) {
+    float r[8];
+    ld8f(p.resid + (long long)row * p.ldr + col, r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += r[j];
+  }
+  const long long ci = (long long)row * p.ldc + col;
+  if (ct == CG_BF16) {
+    st8b((bf16_t*)p.C + ci, v);
+  } else {
+    float* c = (float*)p.C + ci;
+    if (e & CG_EPI_ACCUM) {
+      float o[8];
+      ld8f(c, o);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += o[j];
+    }
+    st8f(c, v);
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_vec_kernel(GemmParams p) {
+  const long long total8 = (long long)p.M * p.N / 8;
+  const long long slab = (long long)p.M * p.N;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total8; i += (long long)gridDim.x * 256) {
+    float s[8], t[8];
+    ld8f(p.ws + i * 8, s);
+    for (int z = 1; z < p.split; ++z) {
+      ld8f(p.ws + z * slab + i * 8, t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += t[j];
+    }
+    const long long e = i * 8;
+    epi_apply8<-1, 0>(p, (int)(e / p.N), (int)(e % p.N), s);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 main loop + epilogue
+// ---------------------------------------------------------------------------
+namespace bfg {
+constexpr int EPI_LD = 68;                     // fp32 staging row stride (conflict-free writes)
+constexpr int EPI_BYTES = 4 * 64 * EPI_LD * 4;  // 4 waves x [64][68] fp32
+constexpr int SMEM = EPI_BYTES > 4 * TILE_BYTES ? EPI_BYTES : 4 * TILE_BYTES;
+}  // namespace bfg
+
+template <bool AK, bool BKC, int EPI, int CT, bool VEC>
+__device__ __forceinline__ void gemm_bf16_body(const GemmParams& p, char* smem) {
   using namespace bfg;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  // images: A0 | A1 | B0 | B1
 #define AS(i) (smem + (i) * TILE_BYTES)
 #define BS(i) (smem + (2 + (i)) * TILE_BYTES)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -266,11 +372,13 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmParams p) {
       for (int i = 0; i < 4; ++i) af[i] = frag<AK>(AS(cur), wm + 16 * i, ks, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j) bfr[j] = frag<BKC>(BS(cur), wn + 16 * j, ks, lane);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     if (more) {
       stage_store<AK>(sa, AS(cur ^ 1), tid);
@@ -278,28 +386,103 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmParams p) {
     }
     __syncthreads();
   }
+#undef AS
+#undef BS
+  if (!VEC) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + v;
+          const int col = n0 + wn + 16 * j + (lane & 15);
+          epi_store(p, row, col, acc[i][j][v]);
+        }
+    return;
+  }
+  // ---- stage the wave's 64x64 fp32 tile through LDS, then 8-column vector epilogue
+  float* st = (float*)smem + wave * 64 * EPI_LD;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + v;
-        const int col = n0 + wn + 16 * j + (lane & 15);
-        epi_store(p, row, col, acc[i][j][v]);
-      }
-#undef AS
-#undef BS
+      for (int v = 0; v < 4; ++v) st[(16 * i + 4 * (lane >> 4) + v) * EPI_LD + 16 * j + (lane & 15)] = acc[i][j][v];
+  __syncthreads();
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int c = lane + 64 * it, r = c >> 3, ch = c & 7;
+    const int row = m0 + wm + r, col = n0 + wn + ch * 8;
+    if (row >= p.M || col >= p.N) continue;
+    float v[8];
+    ld8f(st + r * EPI_LD + ch * 8, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] *= p.alpha;
+    if (p.split > 1) {
+      st8f(p.ws + ((long long)blockIdx.z * p.M + row) * p.N + col, v);
+      continue;
+    }
+    epi_apply8<EPI, CT>(p, row, col, v);
+  }
+}
+
+template <bool AK, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemm_bf16_body<AK, BKC, -1, 0, false>(p, smem);
+}
+
+template <bool AK, bool BKC, int EPI, int CT>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemm_bf16_body<AK, BKC, EPI, CT, true>(p, smem);
 }
 
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
+typedef void (*gemm_kernel_t)(GemmParams);
+
 template <typename K>
 static void launch4(K k00, K k01, K k10, K k11, bool ak, bool bk, dim3 g, dim3 b, size_t sh,
                     hipStream_t s, const GemmParams& p) {
   K k = ak ? (bk ? k11 : k10) : (bk ? k01 : k00);
   hipLaunchKernelGGL(k, g, b, sh, s, p);
+}
+
+// compile-time-specialised epilogues for the combinations the TinyGPT step issues
+static gemm_kernel_t pick_vec(bool ak, bool bk, int e, int ct) {
+#define SPEC(AK_, BK_, E, T) \
+  if (ak == AK_ && bk == BK_ && e == (E) && ct == (T)) return gemm_bf16_vec_kernel<AK_, BK_, (E), (T)>;
+  SPEC(true, true, 0, CG_BF16)
+  SPEC(true, true, 0, CG_F32)
+  SPEC(true, true, CG_EPI_BIAS, CG_BF16)
+  SPEC(true, true, CG_EPI_BIAS | CG_EPI_RESID, CG_F32)
+  SPEC(true, true, CG_EPI_BIAS | CG_EPI_GELU, CG_BF16)
+  SPEC(true, true, CG_EPI_BIAS | CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
+  SPEC(true, true, CG_EPI_RESID, CG_F32)
+  SPEC(true, true, CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
+  SPEC(true, false, 0, CG_BF16)
+  SPEC(true, false, 0, CG_F32)
+  SPEC(true, false, CG_EPI_DGELU, CG_BF16)
+  SPEC(false, false, 0, CG_F32)
+  SPEC(false, false, CG_EPI_ACCUM, CG_F32)
+#undef SPEC
+  if (ak) return bk ? gemm_bf16_vec_kernel<true, true, -1, 0> : gemm_bf16_vec_kernel<true, false, -1, 0>;
+  return bk ? gemm_bf16_vec_kernel<false, true, -1, 0> : gemm_bf16_vec_kernel<false, false, -1, 0>;
+}
+
+static bool vec_ok(const cg_gemm_desc* d, int split) {
+  const int e = d->epilogue;
+  if (d->N % 8 || d->ldc % 8 || ((uintptr_t)d->C & 15)) return false;
+  if ((e & CG_EPI_BIAS) && ((uintptr_t)d->bias & 15)) return false;
+  if ((e & CG_EPI_RESID) && (d->ldr % 8 || ((uintptr_t)d->resid & 15))) return false;
+  if ((e & (CG_EPI_GELU | CG_EPI_DGELU)) &&
+      (d->ld_aux % 8 || ((uintptr_t)((e & CG_EPI_GELU) ? d->aux_out : d->aux) & 15)))
+    return false;
+  if (split > 1 && ((uintptr_t)d->workspace & 15)) return false;
+  return true;
 }
 
 extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
@@ -328,6 +511,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   split = cg_cdiv(d->K > 0 ? d->K : 1, kchunk);
   if (split > 1 && !d->workspace) return CG_EINVAL;
   p.kchunk = kchunk; p.split = split; p.ws = d->workspace;
+  bool vec = false;
 
   if (d->in_dtype == CG_F32) {
     dim3 g(cg_cdiv(p.N, 64), cg_cdiv(p.M, 64), split);
@@ -339,26 +523,32 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     if (d->a_kcontig ? (d->K & 7) : (d->M & 7)) return CG_EUNSUPPORTED;
     if (d->b_kcontig ? (d->K & 7) : (d->N & 7)) return CG_EUNSUPPORTED;
     dim3 g(cg_cdiv(p.N, bfg::BN), cg_cdiv(p.M, bfg::BM), split);
-    const size_t sh = 4 * bfg::TILE_BYTES;
-    static bool attr_done = false;
-    if (!attr_done) {
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, sh);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, sh);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, sh);
-      (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, sh);
-      attr_done = true;
+    const size_t sh = bfg::SMEM;
+    vec = vec_ok(d, split);
+    gemm_kernel_t k;
+    if (vec) {
+      k = pick_vec(d->a_kcontig, d->b_kcontig, split > 1 ? 0 : p.epi, split > 1 ? CG_F32 : p.c_dtype);
+    } else {
+      k = d->a_kcontig ? (d->b_kcontig ? gemm_bf16_kernel<true, true> : gemm_bf16_kernel<true, false>)
+                       : (d->b_kcontig ? gemm_bf16_kernel<false, true> : gemm_bf16_kernel<false, false>);
     }
-    launch4(gemm_bf16_kernel<false, false>, gemm_bf16_kernel<false, true>, gemm_bf16_kernel<true, false>,
-            gemm_bf16_kernel<true, true>, d->a_kcontig, d->b_kcontig, g, dim3(256), sh, s, p);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    hipLaunchKernelGGL(k, g, dim3(256), sh, s, p);
   } else {
     return CG_EUNSUPPORTED;
   }
   CG_LAUNCH_CHECK();
   if (split > 1) {
     const long long total = (long long)p.M * p.N;
-    int blocks = (int)((total + 255) / 256);
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
+    if (vec) {
+      int blocks = (int)((total / 8 + 255) / 256);
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(splitk_reduce_vec_kernel, dim3(blocks), dim3(256), 0, s, p);
+    } else {
+      int blocks = (int)((total + 255) / 256);
+      if (blocks > 4096) blocks = 4096;
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
+    }
     CG_LAUNCH_CHECK();
   }
   return CG_OK;

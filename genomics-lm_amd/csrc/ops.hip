@@ -50,12 +50,81 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// Vectorised fast path: cols = 128*V2, each lane owns V2 float2 pairs at columns
+// 2*(lane + 64 i) (every wave-instruction moves 512 contiguous bytes).
+__device__ __forceinline__ void st2(float* p, float a, float b) { *(float2*)p = make_float2(a, b); }
+__device__ __forceinline__ void st2(bf16_t* p, float a, float b) {
+  *(uint32_t*)p = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+__device__ __forceinline__ float2 ld2(const float* p) { return *(const float2*)p; }
+__device__ __forceinline__ float2 ld2(const bf16_t* p) {
+  const uint32_t u = *(const uint32_t*)p;
+  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u));
+}
+
+template <typename TO, int V2>
+__global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, long long ldx,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  TO* __restrict__ y, long long ldy, float* __restrict__ mean,
+                                                  float* __restrict__ rstd, int rows, float eps) {
+  constexpr int cols = 128 * V2;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (long long)row * ldx;
+  float2 v[V2];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    v[i] = ld2(xr + 2 * (lane + 64 * i));
+    s += v[i].x + v[i].y;
+  }
+  const float mu = wave_sum(s) * (1.0f / cols);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const float a = v[i].x - mu, b = v[i].y - mu;
+    q += a * a + b * b;
+  }
+  const float rs = rsqrtf(wave_sum(q) * (1.0f / cols) + eps);
+  TO* yr = y + (long long)row * ldy;
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    const int c = 2 * (lane + 64 * i);
+    const float2 gm = *(const float2*)(gamma + c), bt = *(const float2*)(beta + c);
+    st2(yr + c, (v[i].x - mu) * rs * gm.x + bt.x, (v[i].y - mu) * rs * gm.y + bt.y);
+  }
+  if (lane == 0) {
+    if (mean) mean[row] = mu;
+    if (rstd) rstd[row] = rs;
+  }
+}
+
+template <typename TO>
+static bool ln_fwd_fast(int V2, dim3 g, hipStream_t s, const float* x, long long ldx, const float* gamma,
+                        const float* beta, TO* y, long long ldy, float* mean, float* rstd, int rows, float eps) {
+#define LNF(N) case N: hipLaunchKernelGGL((ln_fwd_vec<TO, N>), g, dim3(256), 0, s, x, ldx, gamma, beta, y, ldy, mean, rstd, rows, eps); return true;
+  switch (V2) { LNF(1) LNF(2) LNF(3) LNF(4) LNF(6) LNF(8) default: return false; }
+#undef LNF
+}
+
 extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,
                                 const float* beta, void* y, long long ldy, float* mean, float* rstd,
                                 int rows, int cols, float eps, void* stream) {
   if (cols <= 0 || cols > 64 * LN_MAXV || rows < 0) return CG_EUNSUPPORTED;
   if (rows == 0) return CG_OK;
   dim3 g(cg_cdiv(rows, 4));
+  if (cols % 128 == 0 && (ldx % 2) == 0 && (ldy % 2) == 0) {
+    const bool ok = out_dtype == CG_BF16
+                        ? ln_fwd_fast<bf16_t>(cols / 128, g, (hipStream_t)stream, x, ldx, gamma, beta, (bf16_t*)y,
+                                              ldy, mean, rstd, rows, eps)
+                        : ln_fwd_fast<float>(cols / 128, g, (hipStream_t)stream, x, ldx, gamma, beta, (float*)y, ldy,
+                                             mean, rstd, rows, eps);
+    if (ok) {
+      CG_LAUNCH_CHECK();
+      return CG_OK;
+    }
+  }
   if (out_dtype == CG_BF16)
     hipLaunchKernelGGL(ln_fwd_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, x, ldx, gamma, beta,
                        (bf16_t*)y, ldy, mean, rstd, rows, cols, eps);
@@ -67,8 +136,115 @@ extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, co
 }
 
 extern "C" int cg_layernorm_bwd_blocks(int rows) {
-  int b = cg_cdiv(rows, 4);
-  return b > 256 ? 256 : (b < 1 ? 1 : b);
+  int b = cg_cdiv(rows, 16);
+  return b > 1024 ? 1024 : (b < 1 ? 1 : b);
+}
+
+// Vectorised backward: cols = 128*V2; one wave per row, per-lane dgamma/dbeta partials in
+// registers, combined across the block's 4 waves in LDS (fixed order).
+template <typename TD, typename TO, int V2>
+__global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, long long lddy, const float* __restrict__ x,
+                                                  long long ldx, const float* __restrict__ mean,
+                                                  const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                                  const float* __restrict__ g_in, float* __restrict__ g_out,
+                                                  TO* __restrict__ g_out_t, uint32_t seed, uint32_t thr, float dscale,
+                                                  float* __restrict__ partials, int rows) {
+  constexpr int cols = 128 * V2;
+  __shared__ float2 red[4][2 * 64 * V2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = (rows + gridDim.x - 1) / gridDim.x;
+  const int r_begin = blockIdx.x * per, r_end = min(rows, r_begin + per);
+  float2 gm[V2], dg[V2], db[V2];
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    gm[i] = *(const float2*)(gamma + 2 * (lane + 64 * i));
+    dg[i] = make_float2(0.f, 0.f);
+    db[i] = make_float2(0.f, 0.f);
+  }
+  for (int row = r_begin + wave; row < r_end; row += 4) {
+    const float mu = mean[row], rs = rstd[row];
+    const float* xr = x + (long long)row * ldx;
+    const TD* dyr = dy + (long long)row * lddy;
+    float2 xh[V2], gy[V2];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < V2; ++i) {
+      const int c = 2 * (lane + 64 * i);
+      const float2 d = ld2(dyr + c), xv = ld2(xr + c);
+      xh[i] = make_float2((xv.x - mu) * rs, (xv.y - mu) * rs);
+      gy[i] = make_float2(d.x * gm[i].x, d.y * gm[i].y);
+      dg[i].x += d.x * xh[i].x; dg[i].y += d.y * xh[i].y;
+      db[i].x += d.x; db[i].y += d.y;
+      s1 += gy[i].x + gy[i].y;
+      s2 += gy[i].x * xh[i].x + gy[i].y * xh[i].y;
+    }
+    s1 = wave_sum(s1) * (1.0f / cols);
+    s2 = wave_sum(s2) * (1.0f / cols);
+    float* go = g_out + (long long)row * cols;
+    const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
+#pragma unroll
+    for (int i = 0; i < V2; ++i) {
+      const int c = 2 * (lane + 64 * i);
+      float a = rs * (gy[i].x - s1 - xh[i].x * s2), b = rs * (gy[i].y - s1 - xh[i].y * s2);
+      if (gi) {
+        const float2 g2 = ld2(gi + c);
+        a += g2.x; b += g2.y;
+      }
+      st2(go + c, a, b);
+      if (g_out_t) {
+        if (thr) {
+          const uint32_t h = cg_hash_pair(seed, (uint32_t)row, (uint32_t)c >> 1);
+          a = (h & 0xFFFFu) >= thr ? a * dscale : 0.f;
+          b = (h >> 16) >= thr ? b * dscale : 0.f;
+        }
+        st2(g_out_t + (long long)row * cols + c, a, b);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V2; ++i) {
+    red[wave][lane + 64 * i] = dg[i];
+    red[wave][64 * V2 + lane + 64 * i] = db[i];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * 64 * V2; e += 256) {
+    const float2 s = make_float2(red[0][e].x + red[1][e].x + red[2][e].x + red[3][e].x,
+                                 red[0][e].y + red[1][e].y + red[2][e].y + red[3][e].y);
+    const int which = e / (64 * V2), rem = e % (64 * V2);
+    *(float2*)(partials + (long long)blockIdx.x * 2 * cols + which * cols + 2 * rem) = s;
+  }
+}
+
+template <typename TD, typename TO>
+static bool ln_bwd_fast(int V2, int nblk, hipStream_t s, const TD* dy, long long lddy, const float* x, long long ldx,
+                        const float* mean, const float* rstd, const float* gamma, const float* g_in, float* g_out,
+                        TO* g_out_t, uint32_t seed, uint32_t thr, float dscale, float* partials, int rows) {
+#define LNB(N) case N: hipLaunchKernelGGL((ln_bwd_vec<TD, TO, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows); return true;
+  switch (V2) { LNB(1) LNB(2) LNB(3) LNB(4) LNB(6) LNB(8) default: return false; }
+#undef LNB
+}
+
+// sum the per-block partial rows: 64 columns per block, 4 row-interleaved accumulators
+__global__ __launch_bounds__(1024) void ln_param_reduce2(const float* __restrict__ partials, int nblk, int cols,
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         int accumulate) {
+  __shared__ float red[16][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + tx;
+  float s = 0.f;
+  if (c < 2 * cols) {
+#pragma unroll 4
+    for (int b = ty; b < nblk; b += 16) s += partials[(long long)b * 2 * cols + c];
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  if (ty == 0 && c < 2 * cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v += red[i][tx];
+    float* dst = c < cols ? dgamma + c : dbeta + (c - cols);
+    *dst = accumulate ? *dst + v : v;
+  }
 }
 
 // dx = rstd * (dy*g - mean(dy*g) - xhat*mean(dy*g*xhat));  g_out = g_in + dx
@@ -173,6 +349,32 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
   const int nblk = cg_layernorm_bwd_blocks(rows);
   const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   const float dscale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
+  bool fast = false;
+  if (cols % 128 == 0 && cols <= 1024 && (lddy % 2) == 0 && (ldx % 2) == 0) {
+    const int V2 = cols / 128;
+    if (dy_dtype == CG_BF16) {
+      fast = out_dtype == CG_BF16
+                 ? ln_bwd_fast<bf16_t, bf16_t>(V2, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                                               g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows)
+                 : ln_bwd_fast<bf16_t, float>(V2, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                                              g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows);
+    } else {
+      fast = out_dtype == CG_BF16
+                 ? ln_bwd_fast<float, bf16_t>(V2, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                                              g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows)
+                 : ln_bwd_fast<float, float>(V2, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                                             g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows);
+    }
+  }
+  if (fast) {
+    CG_LAUNCH_CHECK();
+    if (dgamma && dbeta) {
+      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv(2 * cols, 64)), dim3(1024), 0, s, partials, nblk, cols, dgamma,
+                         dbeta, accumulate);
+      CG_LAUNCH_CHECK();
+    }
+    return CG_OK;
+  }
 #define LNB(TD, TO)                                                                                  \
   hipLaunchKernelGGL((ln_bwd_kernel<TD, TO>), dim3(nblk), dim3(256), 0, s, (const TD*)dy, lddy, x, ldx, \
                      mean, rstd, gamma, g_in, g_out, (TO*)g_out_t, drop_seed, thr, dscale, partials, rows, cols)
@@ -494,10 +696,69 @@ __global__ void colsum_reduce_kernel(const float* __restrict__ part, int nch, in
   for (int i = 0; i < nch; ++i) s += part[(long long)i * cols + c];
   out[c] = accumulate ? out[c] + s : s;
 }
+// Fast path: 8 columns (one 16-B bf16 chunk / two float4) per thread, 32 column chunks x
+// 8 row lanes per 256-thread block, COLSUM_RB rows per block; partial rows reduced by
+// colsum_reduce_kernel.
+constexpr int COLSUM_RB = 512;
+template <typename T_>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(const T_* __restrict__ X, long long ldx, int rows, int cols,
+                                                         float* __restrict__ part) {
+  __shared__ float red[8][256 + 8];
+  const int ch = threadIdx.x & 31, rs = threadIdx.x >> 5;
+  const int c0 = blockIdx.x * 256 + ch * 8;
+  const int r0 = blockIdx.y * COLSUM_RB;
+  const int r1 = min(rows, r0 + COLSUM_RB);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (c0 < cols) {
+#pragma unroll 4
+    for (int r = r0 + rs; r < r1; r += 8) {
+      const T_* p = X + (long long)r * ldx + c0;
+      if (sizeof(T_) == 2) {
+        const uint4 u = *(const uint4*)p;
+        const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[2 * j] += __uint_as_float(w[j] << 16);
+          acc[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
+        }
+      } else {
+        const float4 a = *(const float4*)p, b = *(const float4*)((const float*)p + 4);
+        acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+        acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rs][ch * 8 + j] = acc[j];
+  __syncthreads();
+  const int c = threadIdx.x;  // one output column per thread
+  if (blockIdx.x * 256 + c < cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += red[i][c];
+    part[(long long)blockIdx.y * cols + blockIdx.x * 256 + c] = v;
+  }
+}
+
 extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out, int accumulate,
                          void* ws, void* stream) {
   if (cols == 0) return CG_OK;
   hipStream_t s = (hipStream_t)stream;
+  const int nrb = cg_cdiv(rows > 0 ? rows : 1, COLSUM_RB);
+  if (cols % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0 && nrb <= COLSUM_R) {
+    dim3 g(cg_cdiv(cols, 256), nrb);
+    if (dtype == CG_BF16)
+      hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)X, ldx, rows, cols, (float*)ws);
+    else
+      hipLaunchKernelGGL(colsum_vec_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, (float*)ws);
+    CG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 256)), dim3(256), 0, s, (const float*)ws, nrb, cols,
+                       out, accumulate);
+    CG_LAUNCH_CHECK();
+    return CG_OK;
+  }
   int nch = COLSUM_R;
   if (nch > rows) nch = rows > 0 ? rows : 1;
   dim3 g(cg_cdiv(cols, 256), nch);

@@ -1,0 +1,5 @@
+set -u
+mkdir -p gpurun_out/prof1
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-kernel-roofline > gpurun_out/prof1/bench.log 2>&1
+echo "rc=$?" >> gpurun_out/prof1/bench.log
