@@ -48,45 +48,18 @@ def flops_per_token(c, V=68):
     return 6 * n_mm + 6 * L * d * T
 
 
-def time_kernel(fn, iters=20):
-    """Average device duration of fn() on the current stream, HIP events around the launches."""
-    fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / iters * 1e-3
-
-
-def kernel_rooflines(c, B, dev):
-    """Live per-kernel timings of the step's dominant kernels at the bench shapes."""
+def probe_pass(kind, run, first, n):
+    """Run n untimed steps with the live probe on `kind`; returns (work, ms, launches)."""
+    import ctypes as C
     from codonlm_amd import _lib as L
-    from codonlm_amd import ops
-    d, T, H = c["n_embd"], c["block_size"], c["n_head"]
-    hd = d // H
-    M = B * T
-    out = {}
-    g = torch.Generator(device="cpu").manual_seed(0)
-    x = torch.randn(M, d, generator=g).to(dev, torch.bfloat16)
-    w1 = (torch.randn(4 * d, d, generator=g) * 0.05).to(dev, torch.bfloat16)
-    b1 = torch.zeros(4 * d, device=dev)
-    aux = torch.empty(M, 4 * d, dtype=torch.bfloat16, device=dev)
-    y = torch.empty(M, 4 * d, dtype=torch.bfloat16, device=dev)
-    t = time_kernel(lambda: ops.gemm(x, w1, out=y, bias=b1, epilogue=L.EPI_BIAS | L.EPI_GELU, aux_out=aux))
-    fl = 2.0 * M * 4 * d * d
-    out["gemm_fc1_fwd"] = dict(bound="mfma", achieved=fl / t / 1e12, peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
-                               ms=t * 1e3, flops=fl)
-    qkv = torch.randn(M, 3 * d, generator=g).to(dev, torch.bfloat16)
-    idx = torch.from_numpy(np.random.default_rng(0).integers(4, 68, size=(B, T))).to(dev)
-    seg = ops.segment_starts(idx, 3)
-    t = time_kernel(lambda: ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=1, drop_p=0.1), iters=10)
-    fl = 4.0 * B * H * hd * T * (T + 1) / 2  # causal-exact QK^T + PV
-    out["attn_fwd"] = dict(bound="mfma", achieved=fl / t / 1e12, peak=PEAK_BF16_TFLOPS, unit="TFLOP/s",
-                           ms=t * 1e3, flops=fl)
-    return out
+    L.lib.cg_probe_enable(kind)
+    for i in range(n):
+        run(first + i)
+    torch.cuda.synchronize()
+    w, ms, k = C.c_double(0), C.c_double(0), C.c_longlong(0)
+    L.check(L.lib.cg_probe_read(C.byref(w), C.byref(ms), C.byref(k)), "cg_probe_read")
+    L.lib.cg_probe_enable(0)
+    return w.value, ms.value, k.value
 
 
 def cpu_baseline(c):
@@ -168,9 +141,25 @@ def main():
     for i in range(args.warmup):
         loss = run(i)
     torch.cuda.synchronize()
+    # find the dominant MFMA kernel with short untimed probe passes (rank-local, no comms)
+    from codonlm_amd import _lib as L
+    probes = {}
+    dominant = 0
+    if not args.no_kernel_roofline and args.dtype == "bf16":
+        nxt = args.warmup
+        for kind in (L.PROBE_GEMM_DW, L.PROBE_GEMM_FWD, L.PROBE_GEMM_DX, L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ,
+                     L.PROBE_ATTN_DKDV):
+            probes[kind] = probe_pass(kind, run, nxt, 2)
+            nxt += 2
+        dominant = max(probes, key=lambda k: probes[k][1])
+        if world > 1:  # all ranks probe the same kernel in the timed region
+            t = torch.tensor([dominant], device=dev)
+            dist.broadcast(t, 0)
+            dominant = int(t.item())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    L.lib.cg_probe_enable(dominant)  # live HIP events around that kernel's launches
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = run(args.warmup + i)
@@ -179,6 +168,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    live = None
+    if dominant:
+        import ctypes as C
+        w, ms, k = C.c_double(0), C.c_double(0), C.c_longlong(0)
+        L.check(L.lib.cg_probe_read(C.byref(w), C.byref(ms), C.byref(k)), "cg_probe_read")
+        L.lib.cg_probe_enable(0)
+        live = (w.value, ms.value, k.value)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -210,15 +206,17 @@ def main():
         "model_flops_per_token": ftok,
         "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),
     }
-    if rank == 0 and not args.no_kernel_roofline and args.dtype == "bf16":
-        ks = kernel_rooflines(c, B, dev)
-        dom = max(ks, key=lambda k: ks[k]["ms"])
-        r = ks[dom]
-        result["roofline"] = {"kernel": dom, "bound": r["bound"], "achieved": round(r["achieved"], 2),
-                              "peak": r["peak"], "unit": r["unit"], "frac": round(r["achieved"] / r["peak"], 4),
-                              "traffic": None}
-        result["kernels"] = {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
-                             for k, v in ks.items()}
+    if rank == 0 and live is not None and live[1] > 0:
+        work, ms, k = live
+        ach = work / (ms * 1e-3) / 1e12
+        result["roofline"] = {"kernel": L.PROBE_NAMES[dominant], "bound": "mfma", "achieved": round(ach, 2),
+                              "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                              "traffic": None, "launches": k, "avg_launch_us": round(ms / k * 1e3, 2),
+                              "measured": "HIP events on the launch stream around every launch in the timed region"}
+        result["kernels"] = {
+            L.PROBE_NAMES[kk]: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None,
+                                "ms_per_step": round(v[1] / 2, 3), "launches_per_step": v[2] // 2}
+            for kk, v in probes.items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(c)
     if rank == 0:

@@ -18,6 +18,10 @@ LIB_PATH = Path(__file__).resolve().parent / "libcodonlm_hip.so"
 CG_F32, CG_BF16 = 0, 1
 CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM = 1, 2, 4, 8, 16, 32
+PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV = range(7)
+PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
+               PROBE_ATTN_FWD: "attn_fwd_mfma", PROBE_ATTN_DQ: "attn_bwd_dq_mfma",
+               PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma"}
 
 # parameter kinds (enum in the header)
 (P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,
@@ -93,6 +97,8 @@ SIGNATURES = {
     "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
     "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),
     "cg_model_hidden": (vp, [C.POINTER(Model), i32, C.POINTER(i32), C.POINTER(i64)]),
+    "cg_probe_enable": (i32, [i32]),
+    "cg_probe_read": (i32, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)]),
     "cg_version": (C.c_char_p, []),
 }
 

@@ -134,6 +134,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
   const bf16_t* vbase = qkv + rowbase * ld + (long long)(H + KV) * hd + (long long)kvh * hd;
   const float c = scale * 1.4426950408889634f;
   const uint32_t drow = (uint32_t)(((long long)b * H + hh) * T + myq);
+  const uint32_t hrow = thr ? cg_row_hash(seed, drow) : 0u;
   const int nks = (hd + 15) >> 4;
 
   float m = -INFINITY, lsum = 0.f;
@@ -166,11 +167,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
       }
       const bool full = (k0 + KT - 1 <= q0w) && (k0 >= w_lo_max);
       if (!full) {
+        const int kq = myq - k0, kl = lo - k0;  // visible iff kl <= key-k0 <= kq
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int key0 = k0 + acc_row(r, lane), key1 = key0 + 32;
-          if (key0 > myq || key0 < lo) s0[r] = -INFINITY;
-          if (key1 > myq || key1 < lo) s1[r] = -INFINITY;
+          const int j0 = acc_row(r, lane), j1 = j0 + 32;
+          s0[r] = (j0 > kq || j0 < kl) ? -INFINITY : s0[r];
+          s1[r] = (j1 > kq || j1 < kl) ? -INFINITY : s1[r];
         }
       }
       float mx = -INFINITY;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
       const float mu = (mn == -INFINITY) ? 0.f : mn;
-      const float alpha = exp2f((m - mu) * c);
+      const float alpha = __builtin_amdgcn_exp2f((m - mu) * c);
       const float mc = mu * c;
       lsum *= alpha;
 #pragma unroll
@@ -190,21 +192,24 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
       float ps = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s0[r] = exp2f(fmaf(s0[r], c, -mc));
-        s1[r] = exp2f(fmaf(s1[r], c, -mc));
+        s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], c, -mc));
+        s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], c, -mc));
         ps += s0[r] + s1[r];
       }
       lsum += ps;
       if (thr) {
+        // colpair of (kb, r) = k0/2 + 2*hl + (r&3)/2 + 4*(r>>2) + 16*kb; the 1/(1-p) scale is
+        // applied once to O at the end
+        const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl) * CG_COLK;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const int key0 = k0 + acc_row(r, lane);
-          const uint32_t h0 = cg_hash_pair(seed, drow, (uint32_t)key0 >> 1);
-          const uint32_t h1 = cg_hash_pair(seed, drow, (uint32_t)(key0 + 32) >> 1);
-          s0[r] = (h0 & 0xFFFFu) >= thr ? s0[r] * dscale : 0.f;
-          s0[r + 1] = (h0 >> 16) >= thr ? s0[r + 1] * dscale : 0.f;
-          s1[r] = (h1 & 0xFFFFu) >= thr ? s1[r] * dscale : 0.f;
-          s1[r + 1] = (h1 >> 16) >= thr ? s1[r + 1] * dscale : 0.f;
+          const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
+          const uint32_t h0 = cg_pair_mix(hb + off * CG_COLK);
+          const uint32_t h1 = cg_pair_mix(hb + (off + 16u) * CG_COLK);
+          s0[r] = (h0 & 0xFFFFu) >= thr ? s0[r] : 0.f;
+          s0[r + 1] = (h0 >> 16) >= thr ? s0[r + 1] : 0.f;
+          s1[r] = (h1 & 0xFFFFu) >= thr ? s1[r] : 0.f;
+          s1[r + 1] = (h1 >> 16) >= thr ? s1[r + 1] : 0.f;
         }
       }
       const v8bf p00 = pack_b(s0, 0), p01 = pack_b(s0, 1), p10 = pack_b(s1, 0), p11 = pack_b(s1, 1);
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
   }
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   if (qok) {
-    const float inv = 1.0f / ltot;
+    const float inv = (thr ? dscale : 1.0f) / ltot;
     bf16_t* yr = y + (rowbase + myq) * ldy + (long long)hh * hd;
 #pragma unroll
     for (int r = 0; r < 16; r += 4) {
@@ -299,6 +304,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
   const bf16_t* kbase = qkv + rowbase * ld + (long long)H * hd + (long long)kvh * hd;
   const bf16_t* vbase = qkv + rowbase * ld + (long long)(H + KV) * hd + (long long)kvh * hd;
   const uint32_t drow = (uint32_t)bhq;
+  const uint32_t hrow = thr ? cg_row_hash(seed, drow) : 0u;
   const int nks = (hd + 15) >> 4;
   v16f a0 = zero16(), a1 = zero16();
   const int t0 = kmin / KT, t1 = kmax / KT;
@@ -330,17 +336,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Vi, kb * 32, ks, lane), df[ks], dp, 0, 0, 0);
           }
         }
+        const int kq = myq - k0 - kb * 32, kl = lo - k0 - kb * 32;
+        const uint32_t hb = hrow + ((uint32_t)((k0 + kb * 32) >> 1) + 2u * (uint32_t)(lane >> 5)) * CG_COLK;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const int key = k0 + kb * 32 + acc_row(r, lane);
-          float p0 = exp2f(fmaf(s[r], c, -lse2)), p1 = exp2f(fmaf(s[r + 1], c, -lse2));
+          const int j = acc_row(r, lane);
+          float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
+          float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c, -lse2));
           if (!full) {
-            if (key > myq || key < lo) p0 = 0.f;
-            if (key + 1 > myq || key + 1 < lo) p1 = 0.f;
+            p0 = (j > kq || j < kl) ? 0.f : p0;
+            p1 = (j + 1 > kq || j + 1 < kl) ? 0.f : p1;
           }
           float d0 = dp[r], d1 = dp[r + 1];
           if (thr) {
-            const uint32_t hsh = cg_hash_pair(seed, drow, (uint32_t)key >> 1);
+            const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
+            const uint32_t hsh = cg_pair_mix(hb + off * CG_COLK);
             d0 = (hsh & 0xFFFFu) >= thr ? d0 * dscale : 0.f;
             d1 = (hsh >> 16) >= thr ? d1 * dscale : 0.f;
           }
@@ -401,7 +411,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   using namespace fa;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per buffer: Q image | dO image | lse2[64] | delta[64] | lo[64]
-  constexpr int BUF = 2 * IMG + 3 * 64 * 4;
+  constexpr int BUF = 2 * IMG + 4 * 64 * 4;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int bk = blockIdx.y, b = bk / KV, kvh = bk % KV;
   const int rep = H / KV;
@@ -422,6 +432,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   }
   const float c = scale * 1.4426950408889634f;
   const int nks = (hd + 15) >> 4;
+  const uint32_t kcol = ((uint32_t)mykey >> 1) * CG_COLK;
   v16f dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
   // query tile range: causal start; stop once every query's segment/window starts after the tile
   const int qt_begin = kt0 / KT;
@@ -447,6 +458,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       fl[tid] = q < T ? lse[bhq] * 1.4426950408889634f : 0.f;
       fl[64 + tid] = q < T ? delta[bhq] : 0.f;
       il[tid] = q < T ? lo_of(seg, rowbase, q, T, window) : 0x7fffffff;
+      il[64 + tid] = thr ? (int)cg_row_hash(seed, (uint32_t)(((long long)b * H + h2) * T + q)) : 0;
     }
   };
   Stage2 sq, sd;
@@ -463,11 +475,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     const float* lse2s = (const float*)(buf + 2 * IMG);
     const float* dls = lse2s + 64;
     const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
+    const uint32_t* hrs = (const uint32_t*)(buf + 2 * IMG + 3 * 64 * 4);
     const bool more = it + 1 < total;
     if (more) stage_load(sq, sd, it + 1);
     const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
     const int q0 = qt * KT;
-    const uint32_t drow0 = (uint32_t)(((long long)b * H + h2) * T);
     // wave activity: some query q in [q0, q0+63] sees some key in [kw0, kw0+31]
     const int qlast = min(T - 1, q0 + KT - 1);
     const bool active = (qlast >= kw0) && (los[0] <= kw0 + 31);
@@ -493,20 +505,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
           const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
           const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+          uint4 hr4 = make_uint4(0, 0, 0, 0);
+          if (thr) hr4 = *(const uint4*)(hrs + qi);
+          const uint32_t hrv[4] = {hr4.x, hr4.y, hr4.z, hr4.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int r = rg + u;
             const int q = q0 + qi + u;
-            float p = exp2f(fmaf(s[r], c, -lv[u]));
-            if (!full && (mykey > q || mykey < lov[u] || q >= T)) p = 0.f;
+            float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[u]));
+            if (!full) p = (mykey > q || mykey < lov[u] || q >= T) ? 0.f : p;
             float d = dp[r];
-            float pdr = p;
+            float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
             if (thr) {
-              const uint32_t hsh = cg_hash_pair(seed, drow0 + (uint32_t)q, (uint32_t)mykey >> 1);
+              const uint32_t hsh = cg_pair_mix(hrv[u] + kcol);
               const uint32_t bits = (mykey & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
               const bool keep = bits >= thr;
               d = keep ? d * dscale : 0.f;
-              pdr = keep ? p * dscale : 0.f;
+              pdr = keep ? p : 0.f;
             }
             pd[r] = pdr;
             s[r] = p * (d - dv4[u]);
@@ -532,6 +547,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   if (kok) {
     bf16_t* kr = dqkv + (rowbase + mykey) * lddq + koff;
     bf16_t* vr = dqkv + (rowbase + mykey) * lddq + voff;
+    const float vs = thr ? dscale : 1.0f;
 #pragma unroll
     for (int r = 0; r < 16; r += 4) {
       const int d0 = acc_row(r, lane);
@@ -540,8 +556,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         w.x = (uint32_t)f2bf(dk0[r] * scale) | ((uint32_t)f2bf(dk0[r + 1] * scale) << 16);
         w.y = (uint32_t)f2bf(dk0[r + 2] * scale) | ((uint32_t)f2bf(dk0[r + 3] * scale) << 16);
         *(uint2*)(kr + d0) = w;
-        w.x = (uint32_t)f2bf(dv0[r]) | ((uint32_t)f2bf(dv0[r + 1]) << 16);
-        w.y = (uint32_t)f2bf(dv0[r + 2]) | ((uint32_t)f2bf(dv0[r + 3]) << 16);
+        w.x = (uint32_t)f2bf(dv0[r] * vs) | ((uint32_t)f2bf(dv0[r + 1] * vs) << 16);
+        w.y = (uint32_t)f2bf(dv0[r + 2] * vs) | ((uint32_t)f2bf(dv0[r + 3] * vs) << 16);
         *(uint2*)(vr + d0) = w;
       }
       if (d0 + 32 < hd) {
@@ -549,8 +565,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         w.x = (uint32_t)f2bf(dk1[r] * scale) | ((uint32_t)f2bf(dk1[r + 1] * scale) << 16);
         w.y = (uint32_t)f2bf(dk1[r + 2] * scale) | ((uint32_t)f2bf(dk1[r + 3] * scale) << 16);
         *(uint2*)(kr + d0 + 32) = w;
-        w.x = (uint32_t)f2bf(dv1[r]) | ((uint32_t)f2bf(dv1[r + 1]) << 16);
-        w.y = (uint32_t)f2bf(dv1[r + 2]) | ((uint32_t)f2bf(dv1[r + 3]) << 16);
+        w.x = (uint32_t)f2bf(dv1[r] * vs) | ((uint32_t)f2bf(dv1[r + 1] * vs) << 16);
+        w.y = (uint32_t)f2bf(dv1[r + 2] * vs) | ((uint32_t)f2bf(dv1[r + 3] * vs) << 16);
         *(uint2*)(vr + d0 + 32) = w;
       }
     }
@@ -568,8 +584,12 @@ static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const in
                                        uint32_t thr, float dscale, float scale, hipStream_t s) {
   dim3 g(cg_cdiv(T, 128), B * H);
   const size_t sh = 4 * fa::IMG;
+  // causal-exact products: QK^T and PV over the T(T+1)/2 visible (q, key) pairs
+  const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
+  cg_probe_begin(CG_PROBE_ATTN_FWD, s);
   hipLaunchKernelGGL(attn_fwd_mfma, g, dim3(256), sh, s, qkv, ld, seg, y, ldy, lse, T, H, KV, hd, window, seed, thr,
                      dscale, scale);
+  cg_probe_end(CG_PROBE_ATTN_FWD, s, 2.0 * tri);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }
@@ -580,13 +600,18 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale, float scale,
                                        hipStream_t s) {
   dim3 gq(cg_cdiv(T, 128), B * H);
+  const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
+  cg_probe_begin(CG_PROBE_ATTN_DQ, s);
   hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse, delta,
                      dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);
+  cg_probe_end(CG_PROBE_ATTN_DQ, s, 3.0 * tri);  // S, dP recomputed + dQ
   CG_LAUNCH_CHECK();
   dim3 gk(cg_cdiv(T, 128), B * KV);
-  const size_t shk = 2 * (2 * fa::IMG + 3 * 64 * 4);
+  const size_t shk = 2 * (2 * fa::IMG + 4 * 64 * 4);
+  cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
   hipLaunchKernelGGL(attn_bwd_dkdv_mfma, gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv, lddq, T,
                      H, KV, hd, window, seed, thr, dscale, scale);
+  cg_probe_end(CG_PROBE_ATTN_DKDV, s, 4.0 * tri);  // S, dP recomputed + dV, dK
   CG_LAUNCH_CHECK();
   return CG_OK;
 }

@@ -5,6 +5,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include "../../include/codonlm_hip.h"
+#include "probe.h"
 
 #define CG_WAVE 64
 
@@ -60,9 +61,18 @@ __device__ __forceinline__ uint32_t cg_fmix32(uint32_t h) {
   h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
   return h;
 }
+// two-stage hash: a full mix per row (hoisted out of inner loops), then one multiply
+// per column pair: pair_mix(row_hash + colpair * K)
+__device__ __forceinline__ uint32_t cg_row_hash(uint32_t seed, uint32_t row) {
+  return cg_fmix32(seed ^ (row * 0x9E3779B1u));
+}
+__device__ __forceinline__ uint32_t cg_pair_mix(uint32_t x) {
+  x ^= x >> 15; x *= 0x2C1B3C6Du; x ^= x >> 12;
+  return x;
+}
+constexpr uint32_t CG_COLK = 0x85EBCA77u;
 __device__ __forceinline__ uint32_t cg_hash_pair(uint32_t seed, uint32_t row, uint32_t colpair) {
-  uint32_t h = (row * 0x9E3779B1u) ^ (colpair * 0x85EBCA77u) ^ seed;
-  return cg_fmix32(h);
+  return cg_pair_mix(cg_row_hash(seed, row) + colpair * CG_COLK);
 }
 __device__ __forceinline__ bool cg_keep(uint32_t seed, uint32_t row, uint32_t col, uint32_t thr) {
   uint32_t h = cg_hash_pair(seed, row, col >> 1);

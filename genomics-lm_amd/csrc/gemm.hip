@@ -533,7 +533,11 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
                        : (d->b_kcontig ? gemm_bf16_kernel<false, true> : gemm_bf16_kernel<false, false>);
     }
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    const int pk = d->a_kcontig ? (d->b_kcontig ? CG_PROBE_GEMM_FWD : CG_PROBE_GEMM_DX)
+                                : (d->b_kcontig ? CG_PROBE_NONE : CG_PROBE_GEMM_DW);
+    cg_probe_begin(pk, s);
     hipLaunchKernelGGL(k, g, dim3(256), sh, s, p);
+    cg_probe_end(pk, s, 2.0 * (double)p.M * (double)p.N * (double)p.K);
   } else {
     return CG_EUNSUPPORTED;
   }

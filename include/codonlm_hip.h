@@ -210,6 +210,22 @@ int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* s
  * L+1 = ln_f output) inside the workspace after a forward; dtype in *dtype_out */
 const void* cg_model_hidden(const cg_model* m, int which, int* dtype_out, long long* ld);
 
+/* Live probe of one kernel class during a real run: HIP events are recorded on the
+ * launching stream around each launch of the selected kernel together with its
+ * algorithmic work (FLOPs for MFMA kernels).  kind 0 disables.  cg_probe_read
+ * synchronises on the recorded events and returns (work, total device ms, launches). */
+enum {
+  CG_PROBE_NONE = 0,
+  CG_PROBE_GEMM_DW = 1,      /* bf16 dW GEMM main kernel (A,B MN-contiguous)       */
+  CG_PROBE_GEMM_FWD = 2,     /* bf16 forward GEMM main kernel (A,B K-contiguous)   */
+  CG_PROBE_GEMM_DX = 3,      /* bf16 dX GEMM main kernel                           */
+  CG_PROBE_ATTN_FWD = 4,     /* attn_fwd_mfma                                      */
+  CG_PROBE_ATTN_DQ = 5,      /* attn_bwd_dq_mfma                                   */
+  CG_PROBE_ATTN_DKDV = 6     /* attn_bwd_dkdv_mfma                                 */
+};
+int cg_probe_enable(int kind);
+int cg_probe_read(double* work, double* ms, long long* launches);
+
 const char* cg_version(void);
 
 #ifdef __cplusplus
