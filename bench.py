@@ -151,7 +151,10 @@ def main():
                      L.PROBE_ATTN_DKDV):
             probes[kind] = probe_pass(kind, run, nxt, 2)
             nxt += 2
-        dominant = max(probes, key=lambda k: probes[k][1])
+        # roofline candidates are single kernels (one rocprof row each); the fwd/dX GEMM classes
+        # span several epilogue specialisations and are reported under "kernels" only
+        single = (L.PROBE_GEMM_DW, L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV)
+        dominant = max(single, key=lambda k: probes[k][1])
         if world > 1:  # all ranks probe the same kernel in the timed region
             t = torch.tensor([dominant], device=dev)
             dist.broadcast(t, 0)
