@@ -72,7 +72,7 @@ SIGNATURES = {
     "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
     "cg_layernorm_bwd_blocks": (i32, [i32]),
     "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, vp, vp,
-                               i32, i32, i32, f32, vp]),
+                               vp, i32, i32, i32, f32, vp]),
     "cg_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, u32, f32, vp]),
     "cg_embed_bwd_workspace": (sz, [i32, i32, i32, i32]),
     "cg_embed_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, u32, f32, i32, vp, vp]),

@@ -78,17 +78,27 @@ def layernorm_fwd(x, weight, bias, out_dtype=torch.float32, eps=1e-5):
     return y, mean, rstd
 
 
-def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5):
+def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5, branch_dtype=None, drop_seed=0, drop_p=0.0):
+    """LayerNorm backward.  With `branch_dtype`, also returns the consumer-branch copy of g_out
+    (dropout-masked with (drop_seed, drop_p)) and its column sums (the producing Linear's bias grad):
+    (g_out, dgamma, dbeta, g_branch, colsum); else (g_out, dgamma, dbeta)."""
     rows, cols = x.shape
     g_out = torch.empty(rows, cols, dtype=torch.float32, device=x.device)
     nblk = L.lib.cg_layernorm_bwd_blocks(rows)
-    part = torch.empty(nblk * 2 * cols, dtype=torch.float32, device=x.device)
+    part = torch.empty(nblk * 3 * cols, dtype=torch.float32, device=x.device)
     dgamma = torch.empty(cols, dtype=torch.float32, device=x.device)
     dbeta = torch.empty_like(dgamma)
+    branch = colsum = None
+    if branch_dtype is not None:
+        branch = torch.empty(rows, cols, dtype=branch_dtype, device=x.device)
+        colsum = torch.empty_like(dgamma)
     L.check(L.lib.cg_layernorm_bwd(_dt(dy), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
-                                   rstd.data_ptr(), weight.data_ptr(), _p(g_in), g_out.data_ptr(), L.CG_F32, None,
-                                   0, 0.0, part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), 0, rows, cols, eps,
-                                   L.stream_ptr(x.device)), "cg_layernorm_bwd")
+                                   rstd.data_ptr(), weight.data_ptr(), _p(g_in), g_out.data_ptr(),
+                                   _dt(branch) if branch is not None else L.CG_F32, _p(branch), drop_seed, drop_p,
+                                   part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _p(colsum), 0, rows, cols,
+                                   eps, L.stream_ptr(x.device)), "cg_layernorm_bwd")
+    if branch_dtype is not None:
+        return g_out, dgamma, dbeta, branch, colsum
     return g_out, dgamma, dbeta
 
 

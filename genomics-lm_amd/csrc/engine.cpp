@@ -189,7 +189,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.g = w.take<float>(M * d * 4);
   A.dtmp = w.take<float>(M * d * 4);
   A.delta = w.take<float>((size_t)B * D.H * T * 4);
-  A.lnpart = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 2 * d * 4);
+  A.lnpart = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
   const long long maxcols = std::max<long long>({big, (long long)d, (long long)D.Hp});
   A.colws = w.take<float>((size_t)64 * maxcols * 4);
   long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,
@@ -428,9 +428,11 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     CK(cg_gemm(&g, C.s));
     float* xL = A.x + (size_t)D.L * M * d;
     const int ll = D.L - 1;
+    // gT feeds block L-1's MLP output Linear: its bias gradient (GELU mode) is gT's column sum
+    float* db2 = (D.L > 0 && !D.swiglu) ? G(C, C.Lo.lay[ll].b2) : nullptr;
     CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xL, d, A.meanf, A.rstdf, P(C, C.Lo.lnfw), nullptr, A.g, C.dt,
                         D.L > 0 ? A.gT : nullptr, site_seed(seed, ll, SITE_MLP), D.L > 0 ? p : 0.f, A.lnpart,
-                        G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), accumulate, (int)M, d, eps, C.s));
+                        G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), db2, accumulate, (int)M, d, eps, C.s));
     return CG_OK;
   }
   if (phase == 1) {
@@ -441,8 +443,8 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     float* xl = A.x + (size_t)l * M * d;
     // ---------------- MLP branch: gT = dL/d(mlp out) (dropout mask applied)
     if (!D.swiglu) {
+      // (b2's gradient was produced by the LayerNorm backward that wrote gT)
       CK(lin_dw(C, A.gT, d, a.g, D.hid, d, D.hid, o.w2, D.hid, accumulate));
-      CK(bias_grad(C, A.gT, d, d, o.b2, accumulate));
       cg_gemm_desc g = lin_dx(C, A.gT, d, o.w2, D.hid, d, D.hid, A.dbig, D.hid);
       g.epilogue = CG_EPI_DGELU; g.aux = a.a; g.ld_aux = D.hid;
       CK(cg_gemm(&g, C.s));
@@ -461,11 +463,11 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       g.c_dtype = CG_F32;
       CK(cg_gemm(&g, C.s));
     }
+    // gT = dL/d(proj out); its column sum is the proj bias gradient
     CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, A.gT, 0, 0.f,
-                        A.lnpart, G(C, o.ln2w), G(C, o.ln2b), accumulate, (int)M, d, eps, C.s));
-    // ---------------- attention branch: gT = dL/d(proj out)
+                        A.lnpart, G(C, o.ln2w), G(C, o.ln2b), G(C, o.bp), accumulate, (int)M, d, eps, C.s));
+    // ---------------- attention branch
     CK(lin_dw(C, A.gT, d, a.y, d, d, d, o.wp, d, accumulate));
-    CK(bias_grad(C, A.gT, d, d, o.bp, accumulate));
     cg_gemm_desc g = lin_dx(C, A.gT, d, o.wp, d, d, d, A.dsmall, d);
     CK(cg_gemm(&g, C.s));
     CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, A.dbig,
@@ -477,9 +479,12 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dtmp, d);
     g.c_dtype = CG_F32;
     CK(cg_gemm(&g, C.s));
+    // gT feeds block l-1's MLP output Linear (bias grad fused as above; lands in block l-1's
+    // gradient range, which is all-reduced only after phase l-1)
+    float* db2 = (l > 0 && !D.swiglu) ? G(C, C.Lo.lay[l - 1].b2) : nullptr;
     CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xl, d, a.mean1, a.rstd1, P(C, o.ln1w), A.g, A.g, C.dt,
                         l > 0 ? A.gT : nullptr, site_seed(seed, l - 1, SITE_MLP), l > 0 ? p : 0.f, A.lnpart,
-                        G(C, o.ln1w), G(C, o.ln1b), accumulate, (int)M, d, eps, C.s));
+                        G(C, o.ln1w), G(C, o.ln1b), db2, accumulate, (int)M, d, eps, C.s));
     return CG_OK;
   }
   if (phase == 2) {

@@ -148,18 +148,19 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
                                                   const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                   const float* __restrict__ g_in, float* __restrict__ g_out,
                                                   TO* __restrict__ g_out_t, uint32_t seed, uint32_t thr, float dscale,
-                                                  float* __restrict__ partials, int rows) {
+                                                  float* __restrict__ partials, int rows, int want_col) {
   constexpr int cols = 128 * V2;
-  __shared__ float2 red[4][2 * 64 * V2];
+  __shared__ float2 red[4][3 * 64 * V2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int per = (rows + gridDim.x - 1) / gridDim.x;
   const int r_begin = blockIdx.x * per, r_end = min(rows, r_begin + per);
-  float2 gm[V2], dg[V2], db[V2];
+  float2 gm[V2], dg[V2], db[V2], dc[V2];
 #pragma unroll
   for (int i = 0; i < V2; ++i) {
     gm[i] = *(const float2*)(gamma + 2 * (lane + 64 * i));
     dg[i] = make_float2(0.f, 0.f);
     db[i] = make_float2(0.f, 0.f);
+    dc[i] = make_float2(0.f, 0.f);
   }
   for (int row = r_begin + wave; row < r_end; row += 4) {
     const float mu = mean[row], rs = rstd[row];
@@ -198,6 +199,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
           b = (h >> 16) >= thr ? b * dscale : 0.f;
         }
         st2(g_out_t + (long long)row * cols + c, a, b);
+        dc[i].x += a; dc[i].y += b;  // column sum of the consumer's dY (its bias gradient)
       }
     }
   }
@@ -205,44 +207,49 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
   for (int i = 0; i < V2; ++i) {
     red[wave][lane + 64 * i] = dg[i];
     red[wave][64 * V2 + lane + 64 * i] = db[i];
+    red[wave][128 * V2 + lane + 64 * i] = dc[i];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 2 * 64 * V2; e += 256) {
+  const int nw = (want_col ? 3 : 2);
+  for (int e = threadIdx.x; e < nw * 64 * V2; e += 256) {
     const float2 s = make_float2(red[0][e].x + red[1][e].x + red[2][e].x + red[3][e].x,
                                  red[0][e].y + red[1][e].y + red[2][e].y + red[3][e].y);
     const int which = e / (64 * V2), rem = e % (64 * V2);
-    *(float2*)(partials + (long long)blockIdx.x * 2 * cols + which * cols + 2 * rem) = s;
+    *(float2*)(partials + (long long)blockIdx.x * nw * cols + which * cols + 2 * rem) = s;
   }
 }
 
 template <typename TD, typename TO>
 static bool ln_bwd_fast(int V2, int nblk, hipStream_t s, const TD* dy, long long lddy, const float* x, long long ldx,
                         const float* mean, const float* rstd, const float* gamma, const float* g_in, float* g_out,
-                        TO* g_out_t, uint32_t seed, uint32_t thr, float dscale, float* partials, int rows) {
-#define LNB(N) case N: hipLaunchKernelGGL((ln_bwd_vec<TD, TO, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows); return true;
+                        TO* g_out_t, uint32_t seed, uint32_t thr, float dscale, float* partials, int rows,
+                        int want_col) {
+#define LNB(N) case N: hipLaunchKernelGGL((ln_bwd_vec<TD, TO, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows, want_col); return true;
   switch (V2) { LNB(1) LNB(2) LNB(3) LNB(4) LNB(6) LNB(8) default: return false; }
 #undef LNB
 }
 
 // sum the per-block partial rows: 64 columns per block, 4 row-interleaved accumulators
+// (nw = 2: dgamma|dbeta, nw = 3: dgamma|dbeta|dcol)
 __global__ __launch_bounds__(1024) void ln_param_reduce2(const float* __restrict__ partials, int nblk, int cols,
-                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         int nw, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta, float* __restrict__ dcol,
                                                          int accumulate) {
   __shared__ float red[16][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + tx;
   float s = 0.f;
-  if (c < 2 * cols) {
+  if (c < nw * cols) {
 #pragma unroll 4
-    for (int b = ty; b < nblk; b += 16) s += partials[(long long)b * 2 * cols + c];
+    for (int b = ty; b < nblk; b += 16) s += partials[(long long)b * nw * cols + c];
   }
   red[ty][tx] = s;
   __syncthreads();
-  if (ty == 0 && c < 2 * cols) {
+  if (ty == 0 && c < nw * cols) {
     float v = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) v += red[i][tx];
-    float* dst = c < cols ? dgamma + c : dbeta + (c - cols);
+    float* dst = c < cols ? dgamma + c : c < 2 * cols ? dbeta + (c - cols) : dcol + (c - 2 * cols);
     *dst = accumulate ? *dst + v : v;
   }
 }
@@ -255,15 +262,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
                                                      const float* __restrict__ gamma, const float* __restrict__ g_in,
                                                      float* __restrict__ g_out, TO* __restrict__ g_out_t,
                                                      uint32_t seed, uint32_t thr, float dscale,
-                                                     float* __restrict__ partials, int rows, int cols) {
-  __shared__ float red[4][2 * 64 * 8];  // per-wave column partials, chunked
+                                                     float* __restrict__ partials, int rows, int cols,
+                                                     int want_col) {
+  __shared__ float red[4][3 * 64 * 8];  // per-wave column partials, chunked
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rows_per_blk = (rows + gridDim.x - 1) / gridDim.x;
   const int r_begin = blockIdx.x * rows_per_blk;
   const int r_end = min(rows, r_begin + rows_per_blk);
-  float dg[LN_MAXV], db[LN_MAXV];
+  float dg[LN_MAXV], db[LN_MAXV], dc[LN_MAXV];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) { dg[i] = 0.f; db[i] = 0.f; }
+  for (int i = 0; i < LN_MAXV; ++i) { dg[i] = 0.f; db[i] = 0.f; dc[i] = 0.f; }
   for (int row = r_begin + wave; row < r_end; row += 4) {
     const float mu = mean[row], rs = rstd[row];
     const float* xr = x + (long long)row * ldx;
@@ -301,6 +309,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
           float w = v;
           if (thr) w = cg_keep(seed, (uint32_t)row, (uint32_t)c, thr) ? w * dscale : 0.f;
           st_act<TO>(got + c, w);
+          dc[i] += w;
         }
       }
     }
@@ -313,37 +322,42 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
     for (int i = 0; i < 8; ++i) {
       red[wave][i * 64 + lane] = dg[cb + i];
       red[wave][512 + i * 64 + lane] = db[cb + i];
+      red[wave][1024 + i * 64 + lane] = dc[cb + i];
     }
     __syncthreads();
-    for (int e = threadIdx.x; e < 1024; e += 256) {
+    const int nw = want_col ? 3 : 2;
+    for (int e = threadIdx.x; e < nw * 512; e += 256) {
       const int which = e >> 9, rem = e & 511, i = rem >> 6, l = rem & 63;
       const int c = l + 64 * (cb + i);
       if (c < cols) {
         const float v = red[0][e] + red[1][e] + red[2][e] + red[3][e];
-        partials[(long long)blockIdx.x * 2 * cols + which * cols + c] = v;
+        partials[(long long)blockIdx.x * nw * cols + which * cols + c] = v;
       }
     }
     __syncthreads();
   }
 }
 
-__global__ void ln_param_reduce_kernel(const float* __restrict__ partials, int nblk, int cols,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta, int accumulate) {
+__global__ void ln_param_reduce_kernel(const float* __restrict__ partials, int nblk, int cols, int nw,
+                                       float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                       float* __restrict__ dcol, int accumulate) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * cols) return;
+  if (c >= nw * cols) return;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partials[(long long)b * 2 * cols + c];
-  float* dst = c < cols ? dgamma + c : dbeta + (c - cols);
+  for (int b = 0; b < nblk; ++b) s += partials[(long long)b * nw * cols + c];
+  float* dst = c < cols ? dgamma + c : c < 2 * cols ? dbeta + (c - cols) : dcol + (c - 2 * cols);
   *dst = accumulate ? *dst + s : s;
 }
 
 extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
                                 const float* mean, const float* rstd, const float* gamma, const float* g_in,
                                 float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
-                                float* partials, float* dgamma, float* dbeta, int accumulate, int rows,
-                                int cols, float eps, void* stream) {
+                                float* partials, float* dgamma, float* dbeta, float* dcolsum, int accumulate,
+                                int rows, int cols, float eps, void* stream) {
   (void)eps;
   if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
+  if (dcolsum && (!g_out_t || !dgamma || !dbeta)) return CG_EINVAL;
+  const int want_col = dcolsum ? 1 : 0;
   if (rows <= 0) return CG_OK;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = cg_layernorm_bwd_blocks(rows);
@@ -355,29 +369,29 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
     if (dy_dtype == CG_BF16) {
       fast = out_dtype == CG_BF16
                  ? ln_bwd_fast<bf16_t, bf16_t>(V2, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
-                                               g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows)
+                                               g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col)
                  : ln_bwd_fast<bf16_t, float>(V2, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
-                                              g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows);
+                                              g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col);
     } else {
       fast = out_dtype == CG_BF16
                  ? ln_bwd_fast<float, bf16_t>(V2, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
-                                              g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows)
+                                              g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col)
                  : ln_bwd_fast<float, float>(V2, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
-                                             g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows);
+                                             g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col);
     }
   }
   if (fast) {
     CG_LAUNCH_CHECK();
     if (dgamma && dbeta) {
-      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv(2 * cols, 64)), dim3(1024), 0, s, partials, nblk, cols, dgamma,
-                         dbeta, accumulate);
+      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 64)), dim3(1024), 0, s, partials, nblk,
+                         cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
       CG_LAUNCH_CHECK();
     }
     return CG_OK;
   }
 #define LNB(TD, TO)                                                                                  \
   hipLaunchKernelGGL((ln_bwd_kernel<TD, TO>), dim3(nblk), dim3(256), 0, s, (const TD*)dy, lddy, x, ldx, \
-                     mean, rstd, gamma, g_in, g_out, (TO*)g_out_t, drop_seed, thr, dscale, partials, rows, cols)
+                     mean, rstd, gamma, g_in, g_out, (TO*)g_out_t, drop_seed, thr, dscale, partials, rows, cols, want_col)
   if (dy_dtype == CG_BF16) {
     if (out_dtype == CG_BF16) LNB(bf16_t, bf16_t); else LNB(bf16_t, float);
   } else {
@@ -386,8 +400,8 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
 #undef LNB
   CG_LAUNCH_CHECK();
   if (dgamma && dbeta) {
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cg_cdiv(2 * cols, 256)), dim3(256), 0, s, partials, nblk,
-                       cols, dgamma, dbeta, accumulate);
+    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cg_cdiv((2 + want_col) * cols, 256)), dim3(256), 0, s, partials,
+                       nblk, cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
     CG_LAUNCH_CHECK();
   }
   return CG_OK;

@@ -65,13 +65,16 @@ int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* 
 /* dx = LN backward(dy) [+ g_in]; writes g_out (fp32) and optionally g_out_t (out_dtype,
  * optionally multiplied by a dropout keep mask (seed,p) for the consumer branch);
  * per-block column partials for dgamma/dbeta go to `partials` [nblk][2*cols]
- * (nblk = cg_layernorm_bwd_blocks(rows)), reduced into dgamma/dbeta (accumulate flag). */
+ * (nblk = cg_layernorm_bwd_blocks(rows)), reduced into dgamma/dbeta (accumulate flag).
+ * dcolsum (optional, needs g_out_t): column sums of g_out_t before rounding = the bias
+ * gradient of the Linear that produced the branch g_out_t feeds (partials then [nblk][3*cols]). */
 int cg_layernorm_bwd_blocks(int rows);
 int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
                      const float* mean, const float* rstd, const float* gamma,
                      const float* g_in, float* g_out, int out_dtype, void* g_out_t,
                      uint32_t drop_seed, float drop_p, float* partials, float* dgamma,
-                     float* dbeta, int accumulate, int rows, int cols, float eps, void* stream);
+                     float* dbeta, float* dcolsum, int accumulate, int rows, int cols, float eps,
+                     void* stream);
 
 /* token + position embedding (+dropout) -- model_tiny_gpt.py:305-312 */
 int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const float* pos_emb, float* x,

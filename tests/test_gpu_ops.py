@@ -105,6 +105,17 @@ def test_layernorm_fwd_bwd(out_dtype, cols):
     assert (go.cpu() - (xr.grad + gin)).abs().max() < 1e-4
     assert (dgam.cpu() - wr.grad).abs().max() < 1e-3
     assert (dbet.cpu() - br.grad).abs().max() < 1e-3
+    # consumer-branch copy (dropout-masked, out_dtype) + its fused column sum (= bias grad)
+    p, seed = 0.2, 777
+    go2, dgam2, dbet2, br_t, csum = ops.layernorm_bwd(dy.to(DEV), x.to(DEV), mean, rstd, w.to(DEV),
+                                                      g_in=gin.to(DEV), branch_dtype=out_dtype,
+                                                      drop_seed=seed, drop_p=p)
+    exp = xr.grad + gin
+    keep = torch.from_numpy(O.dropout_keep(seed, np.arange(rows)[:, None], np.arange(cols)[None, :], p))
+    exp_t = torch.where(keep, exp / (1 - p), torch.zeros(()))
+    assert torch.equal(go2.cpu(), go.cpu()) and torch.equal(dgam2.cpu(), dgam.cpu())
+    assert (br_t.float().cpu() - exp_t).abs().max() < tol * 4 + 1e-4
+    assert (csum.cpu() - exp_t.sum(0)).abs().max() < 2e-3
 
 
 def test_segment_starts():

@@ -1,0 +1,11 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider --timeout=300 > gpurun_out/pytest_gpu.log 2>&1
+rc=$?
+echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1
+rc=$?
+echo "bench rc=$rc" >> gpurun_out/bench.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+bash tools/pmc_gemm.sh
