@@ -439,6 +439,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
   gemm_bf16_body<AK, BKC, EPI, CT, true>(p, smem);
 }
 
+#include "gemm_wide.h"
+
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
@@ -452,9 +454,10 @@ static void launch4(K k00, K k01, K k10, K k11, bool ak, bool bk, dim3 g, dim3 b
 }
 
 // compile-time-specialised epilogues for the combinations the TinyGPT step issues
-static gemm_kernel_t pick_vec(bool ak, bool bk, int e, int ct) {
+template <template <bool, bool, int, int> class KS>
+static gemm_kernel_t pick_spec(bool ak, bool bk, int e, int ct) {
 #define SPEC(AK_, BK_, E, T) \
-  if (ak == AK_ && bk == BK_ && e == (E) && ct == (T)) return gemm_bf16_vec_kernel<AK_, BK_, (E), (T)>;
+  if (ak == AK_ && bk == BK_ && e == (E) && ct == (T)) return KS<AK_, BK_, (E), (T)>::fn;
   SPEC(true, true, 0, CG_BF16)
   SPEC(true, true, 0, CG_F32)
   SPEC(true, true, CG_EPI_BIAS, CG_BF16)
@@ -469,8 +472,35 @@ static gemm_kernel_t pick_vec(bool ak, bool bk, int e, int ct) {
   SPEC(false, false, 0, CG_F32)
   SPEC(false, false, CG_EPI_ACCUM, CG_F32)
 #undef SPEC
-  if (ak) return bk ? gemm_bf16_vec_kernel<true, true, -1, 0> : gemm_bf16_vec_kernel<true, false, -1, 0>;
-  return bk ? gemm_bf16_vec_kernel<false, true, -1, 0> : gemm_bf16_vec_kernel<false, false, -1, 0>;
+  if (ak) return bk ? KS<true, true, -1, 0>::fn : KS<true, false, -1, 0>::fn;
+  return bk ? KS<false, true, -1, 0>::fn : KS<false, false, -1, 0>::fn;
+}
+template <bool AK, bool BKC, int E, int T>
+struct VecK { static constexpr gemm_kernel_t fn = gemm_bf16_vec_kernel<AK, BKC, E, T>; };
+template <bool AK, bool BKC, int E, int T>
+struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC, E, T>; };
+
+// 256x128 LDS-DMA tile: large, 64-aligned K chunks and enough tiles to fill the chip
+static int g_wide_mode = [] {
+  const char* e = getenv("CG_GEMM_WIDE");
+  return e ? atoi(e) : -1;  // -1 auto, 0 never, 1 whenever legal
+}();
+static int wide_mode() { return g_wide_mode; }
+extern "C" int cg_gemm_set_wide(int mode) {
+  const int old = g_wide_mode;
+  g_wide_mode = mode < 0 ? -1 : (mode > 0 ? 1 : 0);
+  return old;
+}
+static bool use_wide(const cg_gemm_desc* d, int kchunk, int split) {
+  const int mode = wide_mode();
+  if (mode == 0) return false;
+  if (d->K % bfw::BKT || kchunk % bfw::BKT || d->M < bfw::BM || d->N < bfw::BN) return false;
+  if (mode == 1) return true;
+  // auto: the LDS-DMA tile wins on K-contiguous operands (forward products); with an
+  // MN-contiguous operand (dX, dW) the 128x128 register-staged tile is still faster
+  if (!d->a_kcontig || !d->b_kcontig) return false;
+  const long long tiles = (long long)cg_cdiv(d->M, bfw::BM) * cg_cdiv(d->N, bfw::BN) * split;
+  return tiles >= 192;
 }
 
 static bool vec_ok(const cg_gemm_desc* d, int split) {
@@ -523,11 +553,18 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     if (d->a_kcontig ? (d->K & 7) : (d->M & 7)) return CG_EUNSUPPORTED;
     if (d->b_kcontig ? (d->K & 7) : (d->N & 7)) return CG_EUNSUPPORTED;
     dim3 g(cg_cdiv(p.N, bfg::BN), cg_cdiv(p.M, bfg::BM), split);
-    const size_t sh = bfg::SMEM;
+    dim3 blk(256);
+    size_t sh = bfg::SMEM;
     vec = vec_ok(d, split);
     gemm_kernel_t k;
-    if (vec) {
-      k = pick_vec(d->a_kcontig, d->b_kcontig, split > 1 ? 0 : p.epi, split > 1 ? CG_F32 : p.c_dtype);
+    const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
+    if (vec && use_wide(d, kchunk, split)) {
+      k = pick_spec<WideK>(d->a_kcontig, d->b_kcontig, ke, kt);
+      g = dim3(cg_cdiv(p.N, bfw::BN) * cg_cdiv(p.M, bfw::BM) * split);
+      blk = dim3(bfw::THREADS);
+      sh = bfw::SMEM;
+    } else if (vec) {
+      k = pick_spec<VecK>(d->a_kcontig, d->b_kcontig, ke, kt);
     } else {
       k = d->a_kcontig ? (d->b_kcontig ? gemm_bf16_kernel<true, true> : gemm_bf16_kernel<true, false>)
                        : (d->b_kcontig ? gemm_bf16_kernel<false, true> : gemm_bf16_kernel<false, false>);
@@ -536,7 +573,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     const int pk = d->a_kcontig ? (d->b_kcontig ? CG_PROBE_GEMM_FWD : CG_PROBE_GEMM_DX)
                                 : (d->b_kcontig ? CG_PROBE_NONE : CG_PROBE_GEMM_DW);
     cg_probe_begin(pk, s);
-    hipLaunchKernelGGL(k, g, dim3(256), sh, s, p);
+    hipLaunchKernelGGL(k, g, blk, sh, s, p);
     cg_probe_end(pk, s, 2.0 * (double)p.M * (double)p.N * (double)p.K);
   } else {
     return CG_EUNSUPPORTED;

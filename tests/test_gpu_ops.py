@@ -231,3 +231,33 @@ def test_adamw_matches_torch():
         ops.adamw_(pd, (grad * 4).to(DEV), m, v, step, [(0, n, 1e-3, 0.05)], shadow=shadow, grad_scale=0.25)
     assert (pd.cpu() - ps.detach()).abs().max() < 1e-6
     assert (shadow.float().cpu() - ps.detach()).abs().max() < 1e-2
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 512), (1000, 200, 192), (256, 136, 1024)])
+def test_gemm_wide_tile(mode, ak, bk, M, N, K):
+    """The 256x128 LDS-DMA tile (forced on) against fp32, incl. partial M/N tiles and split-K."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    g = torch.Generator().manual_seed(M + N + K + 10 * ak + bk)
+    Am = torch.randn(M, K, generator=g)
+    Bn = torch.randn(N, K, generator=g)
+    bias = torch.randn(N, generator=g)
+    a = (Am if ak else Am.t().contiguous()).to(DEV, torch.bfloat16)
+    b = (Bn if bk else Bn.t().contiguous()).to(DEV, torch.bfloat16)
+    ref = _bf(Am) @ _bf(Bn).t()
+    old = L.lib.cg_gemm_set_wide(mode)
+    try:
+        out = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32)
+        outb = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.bfloat16,
+                        bias=bias.to(DEV), epilogue=L.EPI_BIAS)
+        outs = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32,
+                        split_k=2)
+        torch.cuda.synchronize()
+    finally:
+        L.lib.cg_gemm_set_wide(old)
+    tol = 2e-2 * math.sqrt(K)
+    assert (out.cpu() - ref).abs().max().item() <= tol
+    assert (outs.cpu() - ref).abs().max().item() <= tol
+    assert (outb.float().cpu() - (ref + bias)).abs().max().item() <= tol + 0.05 * (ref + bias).abs().max().item()
