@@ -46,6 +46,17 @@ class AdamwSegment(C.Structure):
     _fields_ = [("begin", i64), ("end", i64), ("lr", f32), ("wd", f32)]
 
 
+TRANSPOSE_MAX = 64
+
+
+class TransposeItem(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("dst", C.c_void_p), ("lds", i64), ("ldd", i64), ("rows", i32), ("cols", i32)]
+
+
+class TransposeBatch(C.Structure):
+    _fields_ = [("n", i32), ("items", TransposeItem * TRANSPOSE_MAX)]
+
+
 class ModelCfg(C.Structure):
     _fields_ = [("vocab_size", i32), ("block_size", i32), ("n_layer", i32), ("n_head", i32),
                 ("n_kv_head", i32), ("n_embd", i32), ("use_swiglu", i32), ("use_rope", i32),
@@ -90,6 +101,7 @@ SIGNATURES = {
     "cg_colsum_workspace": (sz, [i32, i32]),
     "cg_colsum": (i32, [i32, vp, i64, i32, i32, vp, i32, vp, vp]),
     "cg_cast_f32_to_bf16": (i32, [vp, vp, i64, vp]),
+    "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),
     "cg_adamw": (i32, [vp, vp, vp, vp, vp, C.POINTER(AdamwSegment), i32, f32, f32, f32, i32, f32, vp]),
     "cg_nonfinite_flag": (i32, [vp, i64, vp, vp]),

@@ -159,3 +159,22 @@ def cast_to_bf16(x):
     L.check(L.lib.cg_cast_f32_to_bf16(x.data_ptr(), out.data_ptr(), x.numel(), L.stream_ptr(x.device)),
             "cg_cast_f32_to_bf16")
     return out.view(x.shape)
+
+
+def transpose16(mats):
+    """Batched transpose of 2-byte 2-D tensors (one launch); returns the contiguous transposes."""
+    if len(mats) > L.TRANSPOSE_MAX:
+        raise ValueError("too many matrices")
+    tb = L.TransposeBatch()
+    tb.n = len(mats)
+    outs = []
+    for i, m in enumerate(mats):
+        if m.element_size() != 2 or m.dim() != 2 or m.stride(1) != 1:
+            raise ValueError("transpose16 takes row-major 2-byte matrices")
+        L.require_device(m, "transpose16")
+        o = torch.empty(m.shape[1], m.shape[0], dtype=m.dtype, device=m.device)
+        tb.items[i] = L.TransposeItem(m.data_ptr(), o.data_ptr(), m.stride(0), o.stride(0), m.shape[0], m.shape[1])
+        outs.append(o)
+    if mats:
+        L.check(L.lib.cg_transpose16_batch(C.byref(tb), L.stream_ptr(mats[0].device)), "cg_transpose16_batch")
+    return outs

@@ -114,8 +114,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
   using namespace fa;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
-  const int qtile = gridDim.x - 1 - blockIdx.x;  // heaviest (latest) query tiles first
+  // grid (B*H, q-tiles): consecutive workgroups are different heads of the same q-tile, so the
+  // round-robin XCD dispatch keeps all q-tiles of one head (its K/V) on one XCD's L2
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
+  const int qtile = gridDim.y - 1 - blockIdx.y;  // heaviest (latest) query tiles first
   const int q0 = qtile * 128, q0w = q0 + wave * 32;
   const int myq = q0w + (lane & 31);
   const bool qok = myq < T;
@@ -271,8 +273,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
   using namespace fa;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int bh = blockIdx.y, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
-  const int qtile = gridDim.x - 1 - blockIdx.x;
+  const int bh = blockIdx.x, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
+  const int qtile = gridDim.y - 1 - blockIdx.y;
   const int q0 = qtile * 128, q0w = q0 + wave * 32;
   const int myq = q0w + (lane & 31);
   const bool qok = myq < T;
@@ -413,9 +415,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   // per buffer: Q image | dO image | lse2[64] | delta[64] | lo[64]
   constexpr int BUF = 2 * IMG + 4 * 64 * 4;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int bk = blockIdx.y, b = bk / KV, kvh = bk % KV;
+  const int bk = blockIdx.x, b = bk / KV, kvh = bk % KV;
   const int rep = H / KV;
-  const int ktile = gridDim.x - 1 - blockIdx.x;  // early keys see the most queries: first
+  const int ktile = gridDim.y - 1 - blockIdx.y;  // early keys see the most queries: first
   const int kt0 = ktile * 128, kw0 = kt0 + wave * 32;
   const int mykey = kw0 + (lane & 31);
   const bool kok = mykey < T;
@@ -582,7 +584,7 @@ static inline bool attn_mfma_supported(int hd, long long ld_in, long long ld_out
 static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, bf16_t* y, long long ldy,
                                        float* lse, int B, int T, int H, int KV, int hd, int window, uint32_t seed,
                                        uint32_t thr, float dscale, float scale, hipStream_t s) {
-  dim3 g(cg_cdiv(T, 128), B * H);
+  dim3 g(B * H, cg_cdiv(T, 128));
   const size_t sh = 4 * fa::IMG;
   // causal-exact products: QK^T and PV over the T(T+1)/2 visible (q, key) pairs
   const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
@@ -599,14 +601,14 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
                                        float* delta, bf16_t* dqkv, long long lddq, int B, int T, int H, int KV,
                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale, float scale,
                                        hipStream_t s) {
-  dim3 gq(cg_cdiv(T, 128), B * H);
+  dim3 gq(B * H, cg_cdiv(T, 128));
   const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
   cg_probe_begin(CG_PROBE_ATTN_DQ, s);
   hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse, delta,
                      dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);
   cg_probe_end(CG_PROBE_ATTN_DQ, s, 3.0 * tri);  // S, dP recomputed + dQ
   CG_LAUNCH_CHECK();
-  dim3 gk(cg_cdiv(T, 128), B * KV);
+  dim3 gk(B * KV, cg_cdiv(T, 128));
   const size_t shk = 2 * (2 * fa::IMG + 4 * 64 * 4);
   cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
   hipLaunchKernelGGL(attn_bwd_dkdv_mfma, gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv, lddq, T,

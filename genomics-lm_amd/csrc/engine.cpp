@@ -134,6 +134,8 @@ struct WS {
 struct LayerAct {
   float *mean1, *rstd1, *mean2, *rstd2, *lse, *xmid;
   void *h1, *qkv, *y, *h2, *a, *g, *gu, *s;
+  // bf16 mode: per-step transposed copies of the shadow weights (K-contiguous dX operands)
+  void *qkvT, *pT, *w1T, *w2T, *wguT, *wdT;
 };
 struct Acts {
   int32_t* seg;
@@ -145,6 +147,7 @@ struct Acts {
   void *dlogits, *gT, *dbig, *dsmall;
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
   size_t splitws_floats;
+  bool wT;  // transposed weight copies present
 };
 
 constexpr int MAX_SPLIT = 8;
@@ -198,6 +201,22 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.splitws = w.take<float>(A.splitws_floats * 4);
   A.embws = w.take<float>((size_t)32 * D.V * d * 4);
   A.cews = w.take<float>((size_t)(1 + 256) * 4);
+  static const bool wt_env = [] { const char* e = getenv("CG_DX_TRANSPOSE"); return !e || atoi(e) != 0; }();
+  A.wT = wt_env && c->dtype == CG_BF16 && d % 8 == 0 && D.Nqkv % 8 == 0 && D.hid % 8 == 0 && D.Hp % 8 == 0;
+  for (int l = 0; l < D.L; ++l) {
+    auto& a = A.la[l];
+    a.qkvT = a.pT = a.w1T = a.w2T = a.wguT = a.wdT = nullptr;
+    if (!A.wT) continue;
+    a.qkvT = w.take<char>((size_t)d * D.Nqkv * 2);
+    a.pT = w.take<char>((size_t)d * d * 2);
+    if (!D.swiglu) {
+      a.w1T = w.take<char>((size_t)d * D.hid * 2);
+      a.w2T = w.take<char>((size_t)D.hid * d * 2);
+    } else {
+      a.wguT = w.take<char>((size_t)d * 2 * D.Hp * 2);
+      a.wdT = w.take<char>((size_t)D.Hp * d * 2);
+    }
+  }
   return w.off + 256;
 }
 
@@ -260,15 +279,49 @@ cg_gemm_desc lin_fwd(const Ctx& C, const void* x, long long ldx, long long woff,
   g.C = y; g.ldc = ldy;
   return g;
 }
-// dx[M,K] = dy[M,N] . W[N,K]
+// dx[M,K] = dy[M,N] . W[N,K]   (wT: optional [K][N] copy of W -> K-contiguous operand)
 cg_gemm_desc lin_dx(const Ctx& C, const void* dy, long long lddy, long long woff, long long ldw, int N, int K, void* dx,
-                    long long lddx) {
+                    long long lddx, const void* wT = nullptr) {
   cg_gemm_desc g = gdesc(C);
   g.M = (int)C.M; g.N = K; g.K = N;
   g.A = dy; g.lda = lddy; g.a_kcontig = 1;
-  g.B = W(C, woff); g.ldb = ldw; g.b_kcontig = 0;
+  if (wT) {
+    g.B = wT; g.ldb = N; g.b_kcontig = 1;
+  } else {
+    g.B = W(C, woff); g.ldb = ldw; g.b_kcontig = 0;
+  }
   g.C = dx; g.ldc = lddx;
   return g;
+}
+// refresh the transposed weight copies of every block (one batched launch per 64 matrices)
+int transpose_weights(const Ctx& C) {
+  if (!C.A.wT) return CG_OK;
+  const Dims& D = C.D;
+  const int d = D.d;
+  cg_transpose_batch tb;
+  tb.n = 0;
+  auto add = [&](long long off, long long ld, int rows, int cols, void* dst) -> int {
+    if (tb.n == CG_TRANSPOSE_MAX) {
+      CK(cg_transpose16_batch(&tb, C.s));
+      tb.n = 0;
+    }
+    tb.items[tb.n++] = cg_transpose_item{W(C, off), dst, ld, rows, rows, cols};
+    return CG_OK;
+  };
+  for (int l = 0; l < D.L; ++l) {
+    const auto& o = C.Lo.lay[l];
+    const auto& a = C.A.la[l];
+    CK(add(o.wqkv, d, D.Nqkv, d, a.qkvT));
+    CK(add(o.wp, d, d, d, a.pT));
+    if (!D.swiglu) {
+      CK(add(o.w1, d, D.hid, d, a.w1T));
+      CK(add(o.w2, D.hid, d, D.hid, a.w2T));
+    } else {
+      CK(add(o.wgu, d, 2 * D.Hp, d, a.wguT));
+      CK(add(o.wd, D.Hp, d, D.Hp, a.wdT));
+    }
+  }
+  return cg_transpose16_batch(&tb, C.s);
 }
 int pick_split(const Ctx& C, int Mo, int N, long long K) {
   const int bm = C.dt == CG_BF16 ? 128 : 64;
@@ -410,6 +463,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   const uint32_t seed = m->seed;
 
   if (phase == 0) {
+    CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
     // d(head weight) = dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero)
     cg_gemm_desc g = gdesc(C);
@@ -445,21 +499,21 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (!D.swiglu) {
       // (b2's gradient was produced by the LayerNorm backward that wrote gT)
       CK(lin_dw(C, A.gT, d, a.g, D.hid, d, D.hid, o.w2, D.hid, accumulate));
-      cg_gemm_desc g = lin_dx(C, A.gT, d, o.w2, D.hid, d, D.hid, A.dbig, D.hid);
+      cg_gemm_desc g = lin_dx(C, A.gT, d, o.w2, D.hid, d, D.hid, A.dbig, D.hid, a.w2T);
       g.epilogue = CG_EPI_DGELU; g.aux = a.a; g.ld_aux = D.hid;
       CK(cg_gemm(&g, C.s));
       CK(lin_dw(C, A.dbig, D.hid, a.h2, d, D.hid, d, o.w1, d, accumulate));
       CK(bias_grad(C, A.dbig, D.hid, D.hid, o.b1, accumulate));
-      g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dtmp, d);
+      g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dtmp, d, a.w1T);
       g.c_dtype = CG_F32;
       CK(cg_gemm(&g, C.s));
     } else {
       CK(lin_dw(C, A.gT, d, a.s, D.Hp, d, D.Hp, o.wd, D.Hp, accumulate));
-      cg_gemm_desc g = lin_dx(C, A.gT, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp);
+      cg_gemm_desc g = lin_dx(C, A.gT, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp, a.wdT);
       CK(cg_gemm(&g, C.s));
       CK(cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, A.dbig, 2 * D.Hp, (int)M, D.hid, C.s));
       CK(lin_dw(C, A.dbig, 2 * D.Hp, a.h2, d, 2 * D.Hp, d, o.wgu, d, accumulate));
-      g = lin_dx(C, A.dbig, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dtmp, d);
+      g = lin_dx(C, A.dbig, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dtmp, d, a.wguT);
       g.c_dtype = CG_F32;
       CK(cg_gemm(&g, C.s));
     }
@@ -468,7 +522,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
                         A.lnpart, G(C, o.ln2w), G(C, o.ln2b), G(C, o.bp), accumulate, (int)M, d, eps, C.s));
     // ---------------- attention branch
     CK(lin_dw(C, A.gT, d, a.y, d, d, d, o.wp, d, accumulate));
-    cg_gemm_desc g = lin_dx(C, A.gT, d, o.wp, d, d, d, A.dsmall, d);
+    cg_gemm_desc g = lin_dx(C, A.gT, d, o.wp, d, d, d, A.dsmall, d, a.pT);
     CK(cg_gemm(&g, C.s));
     CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, A.dbig,
                    D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, A.delta, C.s));
@@ -476,7 +530,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(cg_rope_tab(C.dt, A.dbig, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
     CK(lin_dw(C, A.dbig, D.Nqkv, a.h1, d, D.Nqkv, d, o.wqkv, d, accumulate));
     CK(bias_grad(C, A.dbig, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
-    g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dtmp, d);
+    g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dtmp, d, a.qkvT);
     g.c_dtype = CG_F32;
     CK(cg_gemm(&g, C.s));
     // gT feeds block l-1's MLP output Linear (bias grad fused as above; lands in block l-1's

@@ -4,6 +4,7 @@
 // coalesced lane-strided access, cross-row reductions go through per-block partial
 // slabs reduced in a fixed order (bitwise reproducible, no float atomics).
 #include "common.h"
+#include <algorithm>
 
 // ===========================================================================
 // LayerNorm  (nn.LayerNorm(d), eps=1e-5, biased variance; model_tiny_gpt.py:137-152,216)
@@ -990,6 +991,60 @@ extern "C" int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n,
   int blocks = (int)((n + 255) / 256);
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(cast_b2f_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)src, dst, n);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// Batched 2-byte transpose (bf16 weight matrices -> K-contiguous operands for the
+// backward dX products, so they run on the LDS-DMA tile).  64x64 tiles through LDS,
+// 16-B global accesses on both sides.
+// ===========================================================================
+__global__ __launch_bounds__(256) void transpose16_kernel(cg_transpose_batch tb) {
+  __shared__ uint16_t tile[64][64 + 8];
+  const cg_transpose_item& it = tb.items[blockIdx.y];
+  const int tc = (it.cols + 63) >> 6, tr = (it.rows + 63) >> 6;
+  const int tid = threadIdx.x;
+  for (int t = blockIdx.x; t < tc * tr; t += gridDim.x) {
+    const int r0 = (t / tc) * 64, c0 = (t % tc) * 64;
+    const uint16_t* src = (const uint16_t*)it.src;
+    uint16_t* dst = (uint16_t*)it.dst;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i, r = e >> 3, c = (e & 7) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r0 + r < it.rows && c0 + c < it.cols) v = *(const uint4*)(src + (long long)(r0 + r) * it.lds + c0 + c);
+      const uint16_t* pv = (const uint16_t*)&v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tile[r][c + j] = pv[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i, c = e >> 3, r = (e & 7) * 8;  // dst row = source column
+      if (c0 + c < it.cols && r0 + r < it.rows) {
+        uint16_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = tile[r + j][c];
+        *(uint4*)(dst + (long long)(c0 + c) * it.ldd + r0 + r) = *(const uint4*)w;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int cg_transpose16_batch(const cg_transpose_batch* tb, void* stream) {
+  if (!tb || tb->n < 0 || tb->n > CG_TRANSPOSE_MAX) return CG_EINVAL;
+  if (tb->n == 0) return CG_OK;
+  int maxt = 0;
+  for (int i = 0; i < tb->n; ++i) {
+    const cg_transpose_item& it = tb->items[i];
+    if (it.rows < 0 || it.cols < 0 || !it.src || !it.dst) return CG_EINVAL;
+    if ((it.rows & 7) || (it.cols & 7) || (it.lds & 7) || (it.ldd & 7)) return CG_EUNSUPPORTED;
+    if (((uintptr_t)it.src & 15) || ((uintptr_t)it.dst & 15)) return CG_EUNSUPPORTED;
+    maxt = std::max(maxt, cg_cdiv(it.rows, 64) * cg_cdiv(it.cols, 64));
+  }
+  hipLaunchKernelGGL(transpose16_kernel, dim3(std::min(maxt, 1024), tb->n), dim3(256), 0, (hipStream_t)stream, *tb);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }

@@ -136,6 +136,21 @@ size_t cg_colsum_workspace(int rows, int cols);
 int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out,
               int accumulate, void* ws, void* stream);
 
+/* batched transpose of 2-byte matrices: dst[c][r] = src[r][c]; rows, cols, lds, ldd multiples
+ * of 8, 16-B aligned pointers.  Used to give the backward dX products K-contiguous weight
+ * operands (bf16 shadow weights transposed once per step). */
+#define CG_TRANSPOSE_MAX 64
+typedef struct {
+  const void* src; void* dst;
+  long long lds, ldd;
+  int rows, cols;
+} cg_transpose_item;
+typedef struct {
+  int n;
+  cg_transpose_item items[CG_TRANSPOSE_MAX];
+} cg_transpose_batch;
+int cg_transpose16_batch(const cg_transpose_batch* tb, void* stream);
+
 /* elementwise casts / utilities */
 int cg_cast_f32_to_bf16(const float* src, uint16_t* dst, long long n, void* stream);
 int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stream);

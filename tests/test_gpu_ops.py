@@ -261,3 +261,13 @@ def test_gemm_wide_tile(mode, ak, bk, M, N, K):
     assert (out.cpu() - ref).abs().max().item() <= tol
     assert (outs.cpu() - ref).abs().max().item() <= tol
     assert (outb.float().cpu() - (ref + bias)).abs().max().item() <= tol + 0.05 * (ref + bias).abs().max().item()
+
+
+def test_transpose16_batch():
+    ops = _ops()
+    g = torch.Generator().manual_seed(5)
+    mats = [torch.randn(r, c, generator=g).to(DEV, torch.bfloat16) for r, c in [(1536, 512), (72, 200), (8, 8), (520, 64)]]
+    mats.append(torch.randn(64, 1408, generator=g).to(DEV, torch.bfloat16)[:, :1368])  # strided view
+    outs = ops.transpose16(mats)
+    for m, o in zip(mats, outs):
+        assert torch.equal(o.cpu(), m.cpu().t())
