@@ -13,7 +13,8 @@ from pathlib import Path
 
 import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
 
-LIB_PATH = Path(__file__).resolve().parent / "libcodonlm_hip.so"
+# CG_LIB_PATH: load another build of the same library (same-box A/B of two builds)
+LIB_PATH = Path(os.environ.get("CG_LIB_PATH") or Path(__file__).resolve().parent / "libcodonlm_hip.so")
 
 CG_F32, CG_BF16 = 0, 1
 CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3

@@ -103,6 +103,13 @@ __device__ __forceinline__ float dgelu_f(float x) {
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 
 // host-side launch check
+// bijective remap of a linear workgroup id so that the ids one XCD receives (round-robin
+// dispatch: XCD = id mod 8) become one contiguous logical range (MI355X_MICROARCH guide)
+__device__ __forceinline__ int cg_xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
 #define CG_LAUNCH_CHECK()                                   \
   do {                                                      \
     hipError_t _e = hipGetLastError();                      \

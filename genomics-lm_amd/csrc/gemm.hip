@@ -54,11 +54,11 @@ __device__ __forceinline__ void epi_apply(const GemmParams& p, int row, int col,
   }
 }
 
-__device__ __forceinline__ void epi_store(const GemmParams& p, int row, int col, float v) {
+__device__ __forceinline__ void epi_store(const GemmParams& p, int row, int col, float v, int z) {
   if (row >= p.M || col >= p.N) return;
   v *= p.alpha;
   if (p.split > 1) {
-    p.ws[((long long)blockIdx.z * p.M + row) * p.N + col] = v;
+    p.ws[((long long)z * p.M + row) * p.N + col] = v;
     return;
   }
   epi_apply(p, row, col, v);
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
       for (int v = 0; v < 4; ++v) {
         const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + v;
         const int col = n0 + wn + 16 * j + (lane & 15);
-        epi_store(p, row, col, acc[i][j][v]);
+        epi_store(p, row, col, acc[i][j][v], blockIdx.z);
       }
 }
 
@@ -336,8 +336,12 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmParams& p, char* smem) 
 #define BS(i) (smem + (2 + (i)) * TILE_BYTES)
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kbeg = blockIdx.z * p.kchunk;
+  // XCD-grouped tile order (n fastest, then m, then the split-K slab)
+  const int nwg = gridDim.x * gridDim.y * gridDim.z;
+  const int wg = cg_xcd_remap(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z), nwg);
+  const int bz = wg / (gridDim.x * gridDim.y), bxy = wg % (gridDim.x * gridDim.y);
+  const int m0 = (bxy / gridDim.x) * BM, n0 = (bxy % gridDim.x) * BN;
+  const int kbeg = bz * p.kchunk;
   const int kend = min(p.K, kbeg + p.kchunk);
   const bf16_t* A = (const bf16_t*)p.A;
   const bf16_t* B = (const bf16_t*)p.B;
@@ -397,7 +401,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmParams& p, char* smem) 
         for (int v = 0; v < 4; ++v) {
           const int row = m0 + wm + 16 * i + 4 * (lane >> 4) + v;
           const int col = n0 + wn + 16 * j + (lane & 15);
-          epi_store(p, row, col, acc[i][j][v]);
+          epi_store(p, row, col, acc[i][j][v], bz);
         }
     return;
   }
@@ -420,7 +424,7 @@ __device__ __forceinline__ void gemm_bf16_body(const GemmParams& p, char* smem) 
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] *= p.alpha;
     if (p.split > 1) {
-      st8f(p.ws + ((long long)blockIdx.z * p.M + row) * p.N + col, v);
+      st8f(p.ws + ((long long)bz * p.M + row) * p.N + col, v);
       continue;
     }
     epi_apply8<EPI, CT>(p, row, col, v);

@@ -49,11 +49,6 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, char* lds, ui
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_ptr_t)lds, 16, voff, 0, 0, 0);
 }
 
-// bijective XCD-grouping remap of a linear workgroup id (MI355X_MICROARCH / cdna guide)
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-}
 }  // namespace bfw
 
 template <bool AK, bool BKC, int EPI, int CT>
@@ -63,7 +58,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_wide_kernel(GemmParams p) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
   const int nwg = tiles_n * tiles_m * p.split;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int wg = cg_xcd_remap(blockIdx.x, nwg);
   const int zt = wg / (tiles_n * tiles_m), rem = wg % (tiles_n * tiles_m);
   const int m0 = (rem / tiles_n) * BM, n0 = (rem % tiles_n) * BN;
   const int kbeg = zt * p.kchunk;
