@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int bk = blockIdx.x, b = bk / KV, kvh = bk % KV;
   const int rep = H / KV;
-  const int ktile = gridDim.y - 1 - blockIdx.y;  // early keys see the most queries: first
+  const int ktile = blockIdx.y;  // early keys see the most queries: dispatched first
   const int kt0 = ktile * 128, kw0 = kt0 + wave * 32;
   const int mykey = kw0 + (lane & 31);
   const bool kok = mykey < T;
@@ -443,10 +443,21 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   const int qt_end = (qend - 1) / KT;  // inclusive
   const int nqt = qt_end - qt_begin + 1;
   const int total = nqt * rep;
+  // the per-query rows (lse, delta, segment start) are prefetched with the tiles: loading
+  // them at store time would expose a global-memory round trip every iteration
+  float pl = 0.f, pdl = 0.f;
+  int plo = 0x7fffffff;
   auto stage_load = [&](Stage2& sq, Stage2& sd, int it) {
     const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
     tile_load(sq, qkv + rowbase * ld + (long long)h2 * hd, ld, qt * KT, T, hd, tid);
     tile_load(sd, dy + rowbase * lddy + (long long)h2 * hd, lddy, qt * KT, T, hd, tid);
+    if (tid < 64) {
+      const int q = qt * KT + tid;
+      const long long bhq = ((long long)b * H + h2) * T + (q < T ? q : 0);
+      pl = q < T ? lse[bhq] : 0.f;
+      pdl = q < T ? delta[bhq] : 0.f;
+      plo = q < T ? lo_of(seg, rowbase, q, T, window) : 0x7fffffff;
+    }
   };
   auto stage_store = [&](const Stage2& sq, const Stage2& sd, int it, char* buf) {
     tile_store(sq, buf, tid);
@@ -454,12 +465,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     if (tid < 64) {
       const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
       const int q = qt * KT + tid;
-      const long long bhq = ((long long)b * H + h2) * T + (q < T ? q : 0);
       float* fl = (float*)(buf + 2 * IMG);
       int* il = (int*)(buf + 2 * IMG + 2 * 64 * 4);
-      fl[tid] = q < T ? lse[bhq] * 1.4426950408889634f : 0.f;
-      fl[64 + tid] = q < T ? delta[bhq] : 0.f;
-      il[tid] = q < T ? lo_of(seg, rowbase, q, T, window) : 0x7fffffff;
+      fl[tid] = pl * 1.4426950408889634f;
+      fl[64 + tid] = pdl;
+      il[tid] = plo;
       il[64 + tid] = thr ? (int)cg_row_hash(seed, (uint32_t)(((long long)b * H + h2) * T + q)) : 0;
     }
   };
@@ -480,7 +490,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     const uint32_t* hrs = (const uint32_t*)(buf + 2 * IMG + 3 * 64 * 4);
     const bool more = it + 1 < total;
     if (more) stage_load(sq, sd, it + 1);
-    const int h2 = kvh * rep + it / nqt, qt = qt_begin + it % nqt;
+    const int qt = qt_begin + it % nqt;
     const int q0 = qt * KT;
     // wave activity: some query q in [q0, q0+63] sees some key in [kw0, kw0+31]
     const int qlast = min(T - 1, q0 + KT - 1);

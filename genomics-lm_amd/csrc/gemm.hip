@@ -470,6 +470,7 @@ static gemm_kernel_t pick_spec(bool ak, bool bk, int e, int ct) {
   SPEC(true, true, CG_EPI_BIAS | CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
   SPEC(true, true, CG_EPI_RESID, CG_F32)
   SPEC(true, true, CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
+  SPEC(true, true, CG_EPI_DGELU, CG_BF16)
   SPEC(true, false, 0, CG_BF16)
   SPEC(true, false, 0, CG_F32)
   SPEC(true, false, CG_EPI_DGELU, CG_BF16)
