@@ -15,6 +15,11 @@
 // the transposed reads (ds_read_b64_tr_b16, 4 rows x 32 cols per half-wave) are
 // bank-conflict free (see dual_off).  Head dims < 64 are zero-padded in the image.
 #pragma once
+#include <type_traits>
+
+#ifndef ATTN_FWD_WPS
+#define ATTN_FWD_WPS 2
+#endif
 
 namespace fa {
 constexpr int HDP = 64;        // padded head dim held in LDS / registers
@@ -104,14 +109,22 @@ __device__ __forceinline__ int lo_of(const int32_t* seg, long long rowbase, int 
 }  // namespace fa
 
 // ============================================================================
-// forward: WG = 4 waves x 32 queries (128), key tiles of 64, K/V double-buffered
+// forward: WG = 4 waves x 32 queries (128), key tiles of 64, K/V double-buffered.
+// Compile-time variants keep the per-tile VALU stream branch-free: DROP (dropout on),
+// the two LDS buffers (addresses fold into immediate offsets) and fully-visible vs
+// masked tiles.  The running max is rescaled lazily: only when some query's max grows
+// by more than 2^8 in the exp2 domain (stale maxima are exact - the same m is used for
+// P, the row sum and the LSE; P <= 256 stays in range).
 // ============================================================================
-__global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, long long ld,
+template <bool DROP, int HD>
+__global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, long long ld,
                                                         const int32_t* __restrict__ seg, bf16_t* __restrict__ y,
                                                         long long ldy, float* __restrict__ lse, int T, int H, int KV,
-                                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale,
-                                                        float scale) {
+                                                        int hd_rt, int window, uint32_t seed, uint32_t thr,
+                                                        float dscale, float scale) {
   using namespace fa;
+  constexpr int hd = HD;  // head dim is a compile-time constant: k-steps and the second
+  (void)hd_rt;            // output block unroll without branches
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
   // grid (B*H, q-tiles): consecutive workgroups are different heads of the same q-tile, so the
@@ -136,8 +149,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
   const bf16_t* vbase = qkv + rowbase * ld + (long long)(H + KV) * hd + (long long)kvh * hd;
   const float c = scale * 1.4426950408889634f;
   const uint32_t drow = (uint32_t)(((long long)b * H + hh) * T + myq);
-  const uint32_t hrow = thr ? cg_row_hash(seed, drow) : 0u;
-  const int nks = (hd + 15) >> 4;
+  const uint32_t hrow = DROP ? cg_row_hash(seed, drow) : 0u;
+  constexpr int nks = (hd + 15) >> 4;
 
   float m = -INFINITY, lsum = 0.f;
   v16f o0 = zero16(), o1 = zero16();
@@ -148,9 +161,82 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
   tile_store(sk, smem, tid);
   tile_store(sv, smem + IMG, tid);
   __syncthreads();
-  for (int t = t0; t <= t1; ++t) {
-    const int cur = (t - t0) & 1;
-    const char* Ki = smem + cur * 2 * IMG;
+
+  auto body = [&](const char* Ki, const char* Vi, int k0, auto full_c) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(full_c)::value;
+    v16f s0 = zero16(), s1 = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks < nks) {
+        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 0, ks, lane), qf[ks], s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 32, ks, lane), qf[ks], s1, 0, 0, 0);
+      }
+    }
+    if constexpr (!FULL) {
+      const int kq = myq - k0, kl = lo - k0;  // visible iff kl <= key-k0 <= kq
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int j0 = acc_row(r, lane), j1 = j0 + 32;
+        s0[r] = (j0 > kq || j0 < kl) ? -INFINITY : s0[r];
+        s1[r] = (j1 > kq || j1 < kl) ? -INFINITY : s1[r];
+      }
+    }
+    float mx = fmaxf(s0[0], s1[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    // NaN-safe: (-inf) - (-inf) compares false (a fully masked tile never grows m)
+    const bool grow = (mx - m) * c > 8.0f;
+    if (__any(grow)) {
+      const float mn = grow ? mx : m;
+      const float alpha = grow ? __builtin_amdgcn_exp2f((m - mn) * c) : 1.0f;
+      lsum *= alpha;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+      m = mn;
+    }
+    const float mc = (m == -INFINITY ? 0.f : m) * c;
+    float ps = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], c, -mc));
+      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], c, -mc));
+      ps += s0[r] + s1[r];
+    }
+    lsum += ps;
+    if constexpr (DROP) {
+      // colpair of (kb, r) = k0/2 + 2*hl + (r&3)/2 + 4*(r>>2) + 16*kb; the 1/(1-p) scale is
+      // applied once to O at the end
+      const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl) * CG_COLK;
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
+        const uint32_t h0 = cg_pair_mix(hb + off * CG_COLK);
+        const uint32_t h1 = cg_pair_mix(hb + (off + 16u) * CG_COLK);
+        s0[r] = (h0 & 0xFFFFu) >= thr ? s0[r] : 0.f;
+        s0[r + 1] = (h0 >> 16) >= thr ? s0[r + 1] : 0.f;
+        s1[r] = (h1 & 0xFFFFu) >= thr ? s1[r] : 0.f;
+        s1[r + 1] = (h1 >> 16) >= thr ? s1[r + 1] : 0.f;
+      }
+    }
+    const v8bf p00 = pack_b(s0, 0), p01 = pack_b(s0, 1), p10 = pack_b(s1, 0), p11 = pack_b(s1, 1);
+    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 0, lane), p00, o0, 0, 0, 0);
+    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 0, lane), p01, o0, 0, 0, 0);
+    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 0, lane), p10, o0, 0, 0, 0);
+    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 0, lane), p11, o0, 0, 0, 0);
+    if constexpr (hd > 32) {
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 1, lane), p00, o1, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 1, lane), p01, o1, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 1, lane), p10, o1, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 1, lane), p11, o1, 0, 0, 0);
+    }
+  };
+  auto step = [&](auto cur_c, int t) __attribute__((always_inline)) {
+    constexpr int CUR = decltype(cur_c)::value;
+    const char* Ki = smem + CUR * 2 * IMG;
     const char* Vi = Ki + IMG;
     const bool more = t < t1;
     if (more) {
@@ -159,84 +245,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
     }
     const int k0 = t * KT;
     if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
-      v16f s0 = zero16(), s1 = zero16();
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        if (ks < nks) {
-          s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 0, ks, lane), qf[ks], s0, 0, 0, 0);
-          s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 32, ks, lane), qf[ks], s1, 0, 0, 0);
-        }
-      }
-      const bool full = (k0 + KT - 1 <= q0w) && (k0 >= w_lo_max);
-      if (!full) {
-        const int kq = myq - k0, kl = lo - k0;  // visible iff kl <= key-k0 <= kq
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int j0 = acc_row(r, lane), j1 = j0 + 32;
-          s0[r] = (j0 > kq || j0 < kl) ? -INFINITY : s0[r];
-          s1[r] = (j1 > kq || j1 < kl) ? -INFINITY : s1[r];
-        }
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m, mx);
-      const float mu = (mn == -INFINITY) ? 0.f : mn;
-      const float alpha = __builtin_amdgcn_exp2f((m - mu) * c);
-      const float mc = mu * c;
-      lsum *= alpha;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        o0[r] *= alpha;
-        o1[r] *= alpha;
-      }
-      float ps = 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], c, -mc));
-        s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], c, -mc));
-        ps += s0[r] + s1[r];
-      }
-      lsum += ps;
-      if (thr) {
-        // colpair of (kb, r) = k0/2 + 2*hl + (r&3)/2 + 4*(r>>2) + 16*kb; the 1/(1-p) scale is
-        // applied once to O at the end
-        const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl) * CG_COLK;
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
-          const uint32_t h0 = cg_pair_mix(hb + off * CG_COLK);
-          const uint32_t h1 = cg_pair_mix(hb + (off + 16u) * CG_COLK);
-          s0[r] = (h0 & 0xFFFFu) >= thr ? s0[r] : 0.f;
-          s0[r + 1] = (h0 >> 16) >= thr ? s0[r + 1] : 0.f;
-          s1[r] = (h1 & 0xFFFFu) >= thr ? s1[r] : 0.f;
-          s1[r + 1] = (h1 >> 16) >= thr ? s1[r + 1] : 0.f;
-        }
-      }
-      const v8bf p00 = pack_b(s0, 0), p01 = pack_b(s0, 1), p10 = pack_b(s1, 0), p11 = pack_b(s1, 1);
-      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 0, lane), p00, o0, 0, 0, 0);
-      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 0, lane), p01, o0, 0, 0, 0);
-      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 0, lane), p10, o0, 0, 0, 0);
-      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 0, lane), p11, o0, 0, 0, 0);
-      if (hd > 32) {
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 1, lane), p00, o1, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 1, lane), p01, o1, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 1, lane), p10, o1, 0, 0, 0);
-        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 1, lane), p11, o1, 0, 0, 0);
-      }
-      m = mn;
+      if ((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max)) body(Ki, Vi, k0, std::true_type{});
+      else body(Ki, Vi, k0, std::false_type{});
     }
     if (more) {
-      char* nk = smem + (cur ^ 1) * 2 * IMG;
+      char* nk = smem + (CUR ^ 1) * 2 * IMG;
       tile_store(sk, nk, tid);
       tile_store(sv, nk + IMG, tid);
     }
     __syncthreads();
+  };
+  for (int t = t0; t <= t1; t += 2) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 <= t1) step(std::integral_constant<int, 1>{}, t + 1);
   }
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   if (qok) {
-    const float inv = (thr ? dscale : 1.0f) / ltot;
+    const float inv = (DROP ? dscale : 1.0f) / ltot;
     bf16_t* yr = y + (rowbase + myq) * ldy + (long long)hh * hd;
 #pragma unroll
     for (int r = 0; r < 16; r += 4) {
@@ -262,15 +287,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_mfma(const bf16_t* __restrict
 // backward dQ: WG = 4 waves x 32 queries; key tiles of 64 (K, V images)
 // dS^T = P^T o (dP^T - delta),  dQ^T[d][q] += K^T[d][key] dS^T[key][q]
 // ============================================================================
+template <int HD>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, long long ld,
                                                            const int32_t* __restrict__ seg,
                                                            const bf16_t* __restrict__ dy, long long lddy,
                                                            const bf16_t* __restrict__ yo, long long ldy,
                                                            const float* __restrict__ lse,
                                                            float* __restrict__ delta, bf16_t* __restrict__ dqkv,
-                                                           long long lddq, int T, int H, int KV, int hd, int window,
+                                                           long long lddq, int T, int H, int KV, int hd_rt, int window,
                                                            uint32_t seed, uint32_t thr, float dscale, float scale) {
   using namespace fa;
+  constexpr int hd = HD;
+  (void)hd_rt;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int bh = blockIdx.x, b = bh / H, hh = bh % H, kvh = hh / (H / KV);
@@ -307,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
   const bf16_t* vbase = qkv + rowbase * ld + (long long)(H + KV) * hd + (long long)kvh * hd;
   const uint32_t drow = (uint32_t)bhq;
   const uint32_t hrow = thr ? cg_row_hash(seed, drow) : 0u;
-  const int nks = (hd + 15) >> 4;
+  constexpr int nks = (hd + 15) >> 4;
   v16f a0 = zero16(), a1 = zero16();
   const int t0 = kmin / KT, t1 = kmax / KT;
   Stage2 sk, sv;
@@ -362,7 +390,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
         const v8bf b0 = pack_b(s, 0), b1 = pack_b(s, 1);
         a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 0, 0, lane), b0, a0, 0, 0, 0);
         a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 1, 0, lane), b1, a0, 0, 0, 0);
-        if (hd > 32) {
+        if constexpr (hd > 32) {
           a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 0, 1, lane), b0, a1, 0, 0, 0);
           a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 1, 1, lane), b1, a1, 0, 0, 0);
         }
@@ -402,15 +430,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
 //   S = Q K^T, dP = dO V^T (query rows in registers, key on the lane)
 //   dV^T[d][key] += dO^T[d][q] Pd[q][key];  dK^T[d][key] += Q^T[d][q] dS[q][key]
 // ============================================================================
+template <int HD>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __restrict__ qkv, long long ld,
                                                              const int32_t* __restrict__ seg,
                                                              const bf16_t* __restrict__ dy, long long lddy,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta,
                                                              bf16_t* __restrict__ dqkv, long long lddq, int T, int H,
-                                                             int KV, int hd, int window, uint32_t seed, uint32_t thr,
+                                                             int KV, int hd_rt, int window, uint32_t seed, uint32_t thr,
                                                              float dscale, float scale) {
   using namespace fa;
+  constexpr int hd = HD;
+  (void)hd_rt;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per buffer: Q image | dO image | lse2[64] | delta[64] | lo[64]
   constexpr int BUF = 2 * IMG + 4 * 64 * 4;
@@ -433,7 +464,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     vf[ks] = frag_global(vrow, kok, ks, hd, lane);
   }
   const float c = scale * 1.4426950408889634f;
-  const int nks = (hd + 15) >> 4;
+  constexpr int nks = (hd + 15) >> 4;
   const uint32_t kcol = ((uint32_t)mykey >> 1) * CG_COLK;
   v16f dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
   // query tile range: causal start; stop once every query's segment/window starts after the tile
@@ -545,7 +576,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 1, 0, lane), pb1, dv0, 0, 0, 0);
         dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 0, 0, lane), sb0, dk0, 0, 0, 0);
         dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 1, 0, lane), sb1, dk0, 0, 0, 0);
-        if (hd > 32) {
+        if constexpr (hd > 32) {
           dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 0, 1, lane), pb0, dv1, 0, 0, 0);
           dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 1, 1, lane), pb1, dv1, 0, 0, 0);
           dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 0, 1, lane), sb0, dk1, 0, 0, 0);
@@ -599,8 +630,15 @@ static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   // causal-exact products: QK^T and PV over the T(T+1)/2 visible (q, key) pairs
   const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
   cg_probe_begin(CG_PROBE_ATTN_FWD, s);
-  hipLaunchKernelGGL(attn_fwd_mfma, g, dim3(256), sh, s, qkv, ld, seg, y, ldy, lse, T, H, KV, hd, window, seed, thr,
-                     dscale, scale);
+#define FWD(D, HDv)                                                                                          \
+  hipLaunchKernelGGL((attn_fwd_mfma<D, HDv>), g, dim3(256), sh, s, qkv, ld, seg, y, ldy, lse, T, H, KV, hd, window, \
+                     seed, thr, dscale, scale)
+  if (thr) {
+    if (hd == 64) FWD(true, 64); else if (hd == 48) FWD(true, 48); else FWD(true, 32);
+  } else {
+    if (hd == 64) FWD(false, 64); else if (hd == 48) FWD(false, 48); else FWD(false, 32);
+  }
+#undef FWD
   cg_probe_end(CG_PROBE_ATTN_FWD, s, 2.0 * tri);
   CG_LAUNCH_CHECK();
   return CG_OK;
@@ -614,15 +652,21 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   dim3 gq(B * H, cg_cdiv(T, 128));
   const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
   cg_probe_begin(CG_PROBE_ATTN_DQ, s);
-  hipLaunchKernelGGL(attn_bwd_dq_mfma, gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse, delta,
-                     dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);
+#define DQ(HDv)                                                                                                \
+  hipLaunchKernelGGL((attn_bwd_dq_mfma<HDv>), gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse,   \
+                     delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale)
+  if (hd == 64) DQ(64); else if (hd == 48) DQ(48); else DQ(32);
+#undef DQ
   cg_probe_end(CG_PROBE_ATTN_DQ, s, 3.0 * tri);  // S, dP recomputed + dQ
   CG_LAUNCH_CHECK();
   dim3 gk(B * KV, cg_cdiv(T, 128));
   const size_t shk = 2 * (2 * fa::IMG + 4 * 64 * 4);
   cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
-  hipLaunchKernelGGL(attn_bwd_dkdv_mfma, gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv, lddq, T,
-                     H, KV, hd, window, seed, thr, dscale, scale);
+#define DKDV(HDv)                                                                                               \
+  hipLaunchKernelGGL((attn_bwd_dkdv_mfma<HDv>), gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv,     \
+                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale)
+  if (hd == 64) DKDV(64); else if (hd == 48) DKDV(48); else DKDV(32);
+#undef DKDV
   cg_probe_end(CG_PROBE_ATTN_DKDV, s, 4.0 * tri);  // S, dP recomputed + dV, dK
   CG_LAUNCH_CHECK();
   return CG_OK;

@@ -66,8 +66,10 @@ __device__ __forceinline__ uint32_t cg_fmix32(uint32_t h) {
 __device__ __forceinline__ uint32_t cg_row_hash(uint32_t seed, uint32_t row) {
   return cg_fmix32(seed ^ (row * 0x9E3779B1u));
 }
+// (24-bit multiply: v_mul_u32_u24 issues at full rate, v_mul_lo_u32 at quarter rate; the
+// shift-xor before it folds the high bits into the multiplied low 24)
 __device__ __forceinline__ uint32_t cg_pair_mix(uint32_t x) {
-  x ^= x >> 15; x *= 0x2C1B3C6Du; x ^= x >> 12;
+  x ^= x >> 15; x = __umul24(x, 0x2C1B3Du); x ^= x >> 12;
   return x;
 }
 constexpr uint32_t CG_COLK = 0x85EBCA77u;

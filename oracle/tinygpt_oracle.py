@@ -174,11 +174,12 @@ def dropout_keep(seed: int, row: np.ndarray, col: np.ndarray, p: float) -> np.nd
         c = np.asarray(col, dtype=np.uint64).astype(np.uint32)
         r, c = np.broadcast_arrays(r, c)
         # row hash: fmix32(seed ^ row*0x9E3779B1); pair mix: x = rowhash + (col>>1)*0x85EBCA77,
-        # x ^= x>>15; x *= 0x2C1B3C6D; x ^= x>>12   (common.h cg_row_hash / cg_pair_mix)
+        # x ^= x>>15; x = (x & 0xFFFFFF) * 0x2C1B3D (24-bit multiply); x ^= x>>12
+        # (common.h cg_row_hash / cg_pair_mix)
         hr = _fmix32(np.uint32(seed & 0xFFFFFFFF) ^ (r * np.uint32(0x9E3779B1)).astype(np.uint32))
         h = (hr + ((c >> np.uint32(1)) * np.uint32(0x85EBCA77)).astype(np.uint32)).astype(np.uint32)
         h ^= h >> np.uint32(15)
-        h = (h * np.uint32(0x2C1B3C6D)).astype(np.uint32)
+        h = ((h & np.uint32(0xFFFFFF)) * np.uint32(0x2C1B3D)).astype(np.uint32)
         h ^= h >> np.uint32(12)
         bits = np.where((c & np.uint32(1)) == 0, h & np.uint32(0xFFFF), h >> np.uint32(16))
     thr = np.uint32(min(65536, int(round(p * 65536.0))))

@@ -1,0 +1,18 @@
+"""One forward + backward of the C4 attention (dropout 0.1, SEP segments), for PMC passes."""
+import sys
+from pathlib import Path
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "genomics-lm_amd"))
+import torch
+from codonlm_amd import ops
+
+B, H, T, hd = 16, 8, 1024, 64
+g = torch.Generator().manual_seed(0)
+qkv = (torch.randn(B * T, 3 * H * hd, generator=g) * 0.5).to("cuda", torch.bfloat16)
+idx = torch.randint(4, 68, (B, T), generator=g)
+seg = ops.segment_starts(idx.to("cuda"), 3)
+for _ in range(2):
+    y, lse = ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=5, drop_p=0.1)
+    dy = torch.randn_like(y)
+    ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, H, hd, drop_seed=5, drop_p=0.1)
+torch.cuda.synchronize()
+print("ok")
