@@ -104,6 +104,30 @@ __device__ __forceinline__ float dgelu_f(float x) {
 }
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
 
+// bf16-mode GELU: Phi(x) from Abramowitz-Stegun 7.1.26 (|erf error| <= 1.5e-7, far below the
+// bf16 rounding of the output), one exp2 + one rcp instead of the ocml erff call.  The
+// Gaussian factor e^{-x^2/2} is shared by Phi and the pdf, so dGELU costs one exp as well.
+// (fp32 parity mode keeps gelu_f / dgelu_f above.)
+__device__ __forceinline__ float gelu_phi_q(float x, float& e) {
+  e = __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);  // e^{-x^2/2}
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.23164189992f, fabsf(x), 1.0f));  // p/sqrt(2) = 0.3275911/1.41421
+  float poly = fmaf(t, 1.061405429f, -1.453152027f);
+  poly = fmaf(t, poly, 1.421413741f);
+  poly = fmaf(t, poly, -0.284496736f);
+  poly = fmaf(t, poly, 0.254829592f);
+  const float q = 0.5f * t * poly * e;  // = 0.5 * erfc(|x|/sqrt2)
+  return x >= 0.f ? 1.0f - q : q;       // Phi(x)
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+  float e;
+  return x * gelu_phi_q(x, e);
+}
+__device__ __forceinline__ float dgelu_fast(float x) {
+  float e;
+  const float phi = gelu_phi_q(x, e);
+  return fmaf(x * 0.39894228040143268f, e, phi);
+}
+
 // host-side launch check
 // bijective remap of a linear workgroup id so that the ids one XCD receives (round-robin
 // dispatch: XCD = id mod 8) become one contiguous logical range (MI355X_MICROARCH guide)

@@ -266,14 +266,14 @@ __device__ __forceinline__ void epi_apply8(const GemmParams& p, int row, int col
     if (ct == CG_BF16) st8b((bf16_t*)p.aux_out + ai, v);
     else st8f((float*)p.aux_out + ai, v);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j]);
+    for (int j = 0; j < 8; ++j) v[j] = gelu_fast(v[j]);
   }
   if (e & CG_EPI_DGELU) {
     float a[8];
     if (ct == CG_BF16) ld8b((const bf16_t*)p.aux + ai, a);
     else ld8f((const float*)p.aux + ai, a);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= dgelu_f(a[j]);
+    for (int j = 0; j < 8; ++j) v[j] *= dgelu_fast(a[j]);
   }
   if (e & CG_EPI_DROPOUT) {
 #pragma unroll
