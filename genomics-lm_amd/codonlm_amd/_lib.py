@@ -82,6 +82,7 @@ class Model(C.Structure):
 SIGNATURES = {
     "cg_gemm": (i32, [C.POINTER(GemmDesc), vp]),
     "cg_gemm_set_wide": (i32, [i32]),
+    "cg_gemm_set_pers": (i32, [i32]),
     "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
     "cg_layernorm_bwd_blocks": (i32, [i32]),
     "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, vp, vp,

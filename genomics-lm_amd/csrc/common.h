@@ -22,12 +22,8 @@ typedef short v8s __attribute__((ext_vector_type(8)));
 __device__ __forceinline__ float bf2f(bf16_t h) {
   return __uint_as_float(((uint32_t)h) << 16);
 }
-__device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// hardware v_cvt_pk_bf16_f32 (RNE, NaN stays NaN): no per-element NaN branch
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 
 // Typed load/store of one activation element (T = float or bf16_t).
 template <typename T> __device__ __forceinline__ float ld_act(const T* p);

@@ -12,6 +12,7 @@
 //               MN-contiguous operand -> [k][128] image, ds_read_b64_tr_b16 fragments
 // fp32 path : 64x64x16 tile, v_mfma_f32_16x16x4_f32 (exact fp32 fma chain) -- parity mode.
 #include "common.h"
+#include <algorithm>
 
 struct GemmParams {
   int M, N, K, kchunk;
@@ -444,6 +445,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
 }
 
 #include "gemm_wide.h"
+#include "gemm_pers.h"
 
 // ---------------------------------------------------------------------------
 // host launcher
@@ -484,6 +486,61 @@ template <bool AK, bool BKC, int E, int T>
 struct VecK { static constexpr gemm_kernel_t fn = gemm_bf16_vec_kernel<AK, BKC, E, T>; };
 template <bool AK, bool BKC, int E, int T>
 struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC, E, T>; };
+
+// persistent 256x128 tile (K-contiguous operands only, compile-time epilogues only)
+static gemm_kernel_t pick_pers(int e, int ct) {
+#define PSPEC(E, T) \
+  if (e == (E) && ct == (T)) return gemm_bf16_pers_kernel<(E), (T)>;
+  PSPEC(0, CG_BF16)
+  PSPEC(0, CG_F32)
+  PSPEC(CG_EPI_BIAS, CG_BF16)
+  PSPEC(CG_EPI_BIAS | CG_EPI_RESID, CG_F32)
+  PSPEC(CG_EPI_BIAS | CG_EPI_GELU, CG_BF16)
+  PSPEC(CG_EPI_BIAS | CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
+  PSPEC(CG_EPI_RESID, CG_F32)
+  PSPEC(CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
+  PSPEC(CG_EPI_DGELU, CG_BF16)
+  PSPEC(CG_EPI_ACCUM, CG_F32)
+#undef PSPEC
+  return nullptr;
+}
+static int g_pers_mode = [] {
+  const char* e = getenv("CG_GEMM_PERS");
+  return e ? atoi(e) : 1;  // 1 = persistent tile whenever legal (grid = CUs), 0 = never, N>1: grid capped at N
+}();
+extern "C" int cg_gemm_set_pers(int mode) {
+  const int old = g_pers_mode;
+  g_pers_mode = mode < 0 ? 0 : mode;
+  return old;
+}
+static int cu_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (!n[dev]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n[dev] = v;
+  }
+  return n[dev];
+}
+static bool use_pers(const cg_gemm_desc* d, int split) {
+  if (!g_pers_mode || split != 1) return false;
+  if (!d->a_kcontig || !d->b_kcontig) return false;
+  if (d->K % bfp::BKT || d->K < 2 * bfp::BKT) return false;
+  if (!pick_pers(d->epilogue, d->c_dtype)) return false;
+  // every buffer extent must stay below the out-of-range voffset used for masked lanes
+  const long long lim = (long long)bfp::OOR - (1ll << 24);
+  const long long es = d->c_dtype == CG_BF16 ? 2 : 4;
+  if (((long long)(d->M - 1) * d->lda + d->K) * 2 >= lim) return false;
+  if (((long long)(d->N - 1) * d->ldb + d->K) * 2 >= lim) return false;
+  if (((long long)(d->M - 1) * d->ldc + d->N) * es >= lim) return false;
+  if ((d->epilogue & CG_EPI_RESID) && ((long long)(d->M - 1) * d->ldr + d->N) * 4 >= lim) return false;
+  if ((d->epilogue & (CG_EPI_GELU | CG_EPI_DGELU)) && ((long long)(d->M - 1) * d->ld_aux + d->N) * es >= lim)
+    return false;
+  return true;
+}
 
 // 256x128 LDS-DMA tile: large, 64-aligned K chunks and enough tiles to fill the chip
 static int g_wide_mode = [] {
@@ -563,7 +620,13 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     vec = vec_ok(d, split);
     gemm_kernel_t k;
     const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
-    if (vec && use_wide(d, kchunk, split)) {
+    if (vec && use_pers(d, split)) {
+      k = pick_pers(p.epi, p.c_dtype);
+      const int tiles = cg_cdiv(p.N, bfp::BN) * cg_cdiv(p.M, bfp::BM);
+      g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cu_count()));
+      blk = dim3(bfp::THREADS);
+      sh = bfp::SMEM;
+    } else if (vec && use_wide(d, kchunk, split)) {
       k = pick_spec<WideK>(d->a_kcontig, d->b_kcontig, ke, kt);
       g = dim3(cg_cdiv(p.N, bfw::BN) * cg_cdiv(p.M, bfw::BM) * split);
       blk = dim3(bfw::THREADS);

@@ -1,0 +1,312 @@
+// Persistent bf16 GEMM for the TinyGPT forward and dX products (included by gemm.hip).
+//
+// Both operands K-contiguous, no split-K, K % 64 == 0 and K >= 128.  One 512-thread
+// workgroup per CU walks its tiles (256x128, 8 waves of 64x64, v_mfma_f32_16x16x32_bf16)
+// with ONE LDS-DMA ring (3 stages of 48 KiB) that never drains between tiles: the DMAs of a
+// tile's first two k-steps are issued during the previous tile's last two k-steps, so the
+// pipeline fill and the epilogue of tile i overlap the operand stream of tile i+1.
+//
+// The epilogue needs no LDS.  The MFMA operands are swapped (D = B_frag x A_frag, i.e. the
+// tile is computed transposed) and the B rows are fed in a permuted order, so that after
+// the k-loop every lane owns 16 consecutive output columns of 4 rows (two 8-column chunks):
+// bias / GELU / dGELU / dropout / residual are applied in registers and every global access
+// is a 16-byte buffer load/store.  All epilogue accesses are buffer ops with out-of-range
+// offsets for rows/columns outside the matrix, so every wave issues the same compile-time
+// number of VMEM ops (E) and the counted vmcnt waits of the next tile's first two k-steps
+// can leave the epilogue's stores in flight (vmcnt counts loads, stores and LDS-DMA in
+// issue order).
+namespace bfp {
+using bfw::A_BYTES;
+using bfw::A_CHUNKS;
+using bfw::B_CHUNKS;
+using bfw::BKT;
+using bfw::BM;
+using bfw::BN;
+using bfw::STAGE_BYTES;
+using bfw::STAGES;
+using bfw::THREADS;
+using bfw::WAVES;
+constexpr int SMEM = STAGES * STAGE_BYTES;  // 144 KiB
+constexpr int DMA_PER_STAGE = A_CHUNKS + B_CHUNKS;
+constexpr uint32_t OOR = 0x80000000u;  // voffset past every range used here (host: extents < 2^31 - 2^24)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// B image [128 rows][64 bf16], 16-B chunk `ch` of row r stored at chunk ch ^ fb(r): with the
+// permuted fragment rows below every ds_read_b128 lane group hits 16 distinct bank slots.
+__device__ __forceinline__ int fb(int row) { return (row & 2) | ((row >> 1) & 4); }
+__device__ __forceinline__ uint32_t b_src_off(int pos, long long ld) {
+  const int row = pos >> 7, phys = (pos >> 4) & 7;
+  return (uint32_t)(((long long)row * ld + 8 * (phys ^ fb(row))) * 2);
+}
+// fragment of B for output-column block j (it sits in the MFMA's A slot): lane l supplies the
+// row that makes D[4g+v][l&15] land on column wn + 32(j>>1) + 8g + 4(j&1) + v
+__device__ __forceinline__ v8bf bfrag(const char* img, int wn, int j, int ks, int lane) {
+  const int nl = lane & 15;
+  const int row = wn + 32 * (j >> 1) + 8 * (nl >> 2) + 4 * (j & 1) + (nl & 3);
+  const int ch = ks * 4 + (lane >> 4);
+  return *(const v8bf*)(img + row * 128 + 16 * (ch ^ fb(row)));
+}
+
+template <int EPI, int CT>
+struct Epi {
+  static constexpr int W = CT == CG_BF16 ? 1 : 2;  // 16-B accesses per 8 values of C dtype
+  static constexpr int PER = W + ((EPI & CG_EPI_GELU) ? W : 0) + ((EPI & CG_EPI_DGELU) ? W : 0) +
+                             ((EPI & CG_EPI_RESID) ? 2 : 0) + ((EPI & CG_EPI_ACCUM) ? 2 : 0);
+  static constexpr int E = 8 * PER + ((EPI & CG_EPI_BIAS) ? 4 : 0);  // VMEM ops per wave per epilogue
+};
+
+__device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+__device__ __forceinline__ void unpack_f32(u32x4 a, u32x4 b, float v[8]) {
+  v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
+  v[4] = __uint_as_float(b.x); v[5] = __uint_as_float(b.y); v[6] = __uint_as_float(b.z); v[7] = __uint_as_float(b.w);
+}
+__device__ __forceinline__ void unpack_bf16(u32x4 a, float v[8]) {
+  const uint32_t w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    v[2 * j] = __uint_as_float(w[j] << 16);
+    v[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+}
+__device__ __forceinline__ u32x4 pack_bf16(const float v[8]) {
+  u32x4 u;
+  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return u;
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+}  // namespace bfp
+
+template <int EPI, int CT>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
+  using namespace bfp;
+  constexpr int E = Epi<EPI, CT>::E;
+  constexpr int ES = CT == CG_BF16 ? 2 : 4;
+  static_assert(E + DMA_PER_STAGE <= 63, "vmcnt range");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int ntiles = tiles_n * tiles_m;
+  const int nblk = gridDim.x;
+  const int lb = cg_xcd_remap(blockIdx.x, nblk);  // an XCD's blocks walk contiguous tile ranges
+  const int my_tiles = lb < ntiles ? (ntiles - 1 - lb) / nblk + 1 : 0;
+  const int nt = p.K / BKT;
+  const int S = my_tiles * nt;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+
+  const __amdgpu_buffer_rsrc_t ra = rsrc(p.A, ((long long)(p.M - 1) * p.lda + p.K) * 2);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(p.B, ((long long)(p.N - 1) * p.ldb + p.K) * 2);
+  uint32_t va[A_CHUNKS], vb[B_CHUNKS];
+#pragma unroll
+  for (int i = 0; i < A_CHUNKS; ++i) va[i] = bfw::src_off<true>((wave + WAVES * i) * 1024 + 16 * lane, p.lda);
+#pragma unroll
+  for (int i = 0; i < B_CHUNKS; ++i) vb[i] = b_src_off((wave + WAVES * i) * 1024 + 16 * lane, p.ldb);
+
+  auto tile_org = [&](int k, int& m0, int& n0) {
+    const int tile = lb + k * nblk;
+    m0 = (tile / tiles_n) * BM;
+    n0 = (tile % tiles_n) * BN;
+  };
+  // DMA source origins of global k-step g (OOR past the end: the DMA then fills a free slot with zeros)
+  auto stage_org = [&](int g, uint32_t& ao, uint32_t& bo) {
+    if (g >= S) {
+      ao = bo = OOR;
+      return;
+    }
+    const int k = g / nt, t = g - k * nt;
+    int m0, n0;
+    tile_org(k, m0, n0);
+    ao = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
+    bo = (uint32_t)(((long long)n0 * p.ldb + t * BKT) * 2);
+  };
+  auto issue = [&](int g) {
+    uint32_t ao, bo;
+    stage_org(g, ao, bo);
+    char* st = smem + (g % STAGES) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < A_CHUNKS; ++i) bfw::dma16(ra, st + (wave + WAVES * i) * 1024, ao + va[i]);
+#pragma unroll
+    for (int i = 0; i < B_CHUNKS; ++i) bfw::dma16(rb, st + A_BYTES + (wave + WAVES * i) * 1024, bo + vb[i]);
+  };
+
+  v4f acc[4][4];
+  // one k-step of global index g (the DMAs of stage g+2 interleaved with the MFMAs, as in the
+  // non-persistent 256x128 kernel; they are always issued, so every step carries 6)
+  auto step = [&](int g, bool after_epi) {
+    if (after_epi) wait_vm<DMA_PER_STAGE + E>();
+    else wait_vm<DMA_PER_STAGE>();
+    __builtin_amdgcn_s_barrier();
+    const char* st = smem + (g % STAGES) * STAGE_BYTES;
+    const char* as = st;
+    const char* bs = st + A_BYTES;
+    v8bf af[2][4], bfr[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[0][i] = bfg::frag<true>(as, wm + 16 * i, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[0][j] = bfrag(bs, wn, j, 0, lane);
+    uint32_t ao, bo;
+    stage_org(g + 2, ao, bo);
+    char* nx = smem + ((g + 2) % STAGES) * STAGE_BYTES;
+#pragma unroll
+    for (int gr = 0; gr < 8; ++gr) {
+      const int i = gr >> 1, j0 = 2 * (gr & 1);
+      acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0], af[0][i], acc[i][j0], 0, 0, 0);
+      acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
+      if (gr < 4) af[1][gr] = bfg::frag<true>(as, wm + 16 * gr, 1, lane);
+      else bfr[1][gr - 4] = bfrag(bs, wn, gr - 4, 1, lane);
+      if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
+      else if (gr < A_CHUNKS + B_CHUNKS)
+        bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int gr = 0; gr < 8; ++gr) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      if (gr < A_CHUNKS + B_CHUNKS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+  };
+
+  // epilogue of local tile k straight from the accumulators: lane owns rows
+  // m0+wm+16i+(l&15) (i = 0..3) x columns n0+wn+32c+8(l>>4)+[0,8) (c = 0..1)
+  auto epilogue = [&](int k) {
+    int m0, n0;
+    tile_org(k, m0, n0);
+    const int g4 = lane >> 4, r16 = lane & 15;
+    const __amdgpu_buffer_rsrc_t rc = rsrc(p.C, ((long long)(p.M - 1) * p.ldc + p.N) * ES);
+    int col[2];
+    bool cok[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      col[c] = n0 + wn + 32 * c + 8 * g4;
+      cok[c] = col[c] < p.N;
+    }
+    float bia[2][8];
+    if constexpr ((EPI & CG_EPI_BIAS) != 0) {
+      const __amdgpu_buffer_rsrc_t rbias = rsrc(p.bias, (long long)p.N * 4);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t o = cok[c] ? (uint32_t)col[c] * 4u : OOR;
+        unpack_f32(bld(rbias, o), bld(rbias, o + 16), bia[c]);
+      }
+    }
+    // operand loads for the whole tile first (one wait for all of them)
+    u32x4 xa[4][2], xb[4][2];
+    uint32_t off_c[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + wm + 16 * i + r16;
+      const bool rok = row < p.M;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bool ok = rok && cok[c];
+        off_c[i][c] = ok ? (uint32_t)(((long long)row * p.ldc + col[c]) * ES) : OOR;
+        if constexpr ((EPI & CG_EPI_RESID) != 0) {
+          const __amdgpu_buffer_rsrc_t rr = rsrc(p.resid, ((long long)(p.M - 1) * p.ldr + p.N) * 4);
+          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ldr + col[c]) * 4) : OOR;
+          xa[i][c] = bld(rr, o);
+          xb[i][c] = bld(rr, o + 16);
+        }
+        if constexpr ((EPI & CG_EPI_DGELU) != 0) {
+          const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux, ((long long)(p.M - 1) * p.ld_aux + p.N) * ES);
+          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ld_aux + col[c]) * ES) : OOR;
+          xa[i][c] = bld(rx, o);
+          if constexpr (CT != CG_BF16) xb[i][c] = bld(rx, o + 16);
+        }
+        if constexpr ((EPI & CG_EPI_ACCUM) != 0) {
+          xa[i][c] = bld(rc, off_c[i][c]);
+          xb[i][c] = bld(rc, off_c[i][c] + 16);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + wm + 16 * i + r16;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float v[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[4 * h + u] = acc[i][2 * c + h][u] * p.alpha;
+        if constexpr ((EPI & CG_EPI_BIAS) != 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += bia[c][j];
+        }
+        if constexpr ((EPI & CG_EPI_GELU) != 0) {
+          const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux_out, ((long long)(p.M - 1) * p.ld_aux + p.N) * ES);
+          const uint32_t o = off_c[i][c] == OOR ? OOR : (uint32_t)(((long long)row * p.ld_aux + col[c]) * ES);
+          if constexpr (CT == CG_BF16) {
+            bst(rx, o, pack_bf16(v));
+          } else {
+            bst(rx, o, (u32x4){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+            bst(rx, o + 16, (u32x4){__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = gelu_fast(v[j]);
+        }
+        if constexpr ((EPI & CG_EPI_DGELU) != 0) {
+          float a[8];
+          if constexpr (CT == CG_BF16) unpack_bf16(xa[i][c], a);
+          else unpack_f32(xa[i][c], xb[i][c], a);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= dgelu_fast(a[j]);
+        }
+        if constexpr ((EPI & CG_EPI_DROPOUT) != 0) {
+          const uint32_t rh = cg_row_hash(p.drop_seed, (uint32_t)row);
+#pragma unroll
+          for (int j = 0; j < 8; j += 2) {
+            const uint32_t hsh = cg_pair_mix(rh + ((uint32_t)(col[c] + j) >> 1) * CG_COLK);
+            v[j] = (hsh & 0xFFFFu) >= p.drop_thr ? v[j] * p.drop_scale : 0.f;
+            v[j + 1] = (hsh >> 16) >= p.drop_thr ? v[j + 1] * p.drop_scale : 0.f;
+          }
+        }
+        if constexpr ((EPI & (CG_EPI_RESID | CG_EPI_ACCUM)) != 0) {
+          float r[8];
+          unpack_f32(xa[i][c], xb[i][c], r);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] += r[j];
+        }
+        if constexpr (CT == CG_BF16) {
+          bst(rc, off_c[i][c], pack_bf16(v));
+        } else {
+          bst(rc, off_c[i][c], (u32x4){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
+          bst(rc, off_c[i][c] + 16, (u32x4){__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
+        }
+      }
+    }
+  };
+
+  issue(0);
+  issue(1);
+  int g = 0;
+  for (int k = 0; k < my_tiles; ++k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nt; ++t, ++g) step(g, k > 0 && t < 2);
+    epilogue(k);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
+}

@@ -60,6 +60,11 @@ int cg_gemm(const cg_gemm_desc* d, void* stream);
 /* bf16 tile selection: -1 auto (default; env CG_GEMM_WIDE overrides at load), 0 = 128x128
  * register-staged tile only, 1 = 256x128 LDS-DMA tile whenever legal.  Returns the previous mode. */
 int cg_gemm_set_wide(int mode);
+/* persistent 256x128 tile for K-contiguous, un-split products (forward and dX): 1 = whenever
+ * legal with one workgroup per CU (default; env CG_GEMM_PERS overrides at load), 0 = never,
+ * N > 1 = whenever legal with the grid capped at N workgroups (each walks more tiles).
+ * Returns the previous mode. */
+int cg_gemm_set_pers(int mode);
 
 /* LayerNorm (nn.LayerNorm, biased var, eps) -- model_tiny_gpt.py:137,139,216 */
 int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,

@@ -271,3 +271,55 @@ def test_transpose16_batch():
     outs = ops.transpose16(mats)
     for m, o in zip(mats, outs):
         assert torch.equal(o.cpu(), m.cpu().t())
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256)])
+def test_gemm_persistent_tile_epilogues(cap, M, N, K):
+    """Persistent 256x128 tile (K-contiguous operands): every compile-time epilogue, partial
+    M/N tiles, and (cap=3) a grid of 3 workgroups that each walk many tiles, so the LDS-DMA ring
+    and the counted waits carry across tile boundaries with epilogue stores in flight."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.1
+    bias = torch.randn(N, generator=g)
+    res = torch.randn(M, N, generator=g)
+    xd, wd = x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16)
+    base = _bf(x) @ _bf(w).t()
+    tol = 3e-2 * 4
+    old = L.lib.cg_gemm_set_pers(cap)
+    try:
+        y0 = ops.gemm(xd, wd, out_dtype=torch.float32)
+        y0b = ops.gemm(xd, wd, out_dtype=torch.bfloat16)
+        yb = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV), epilogue=L.EPI_BIAS)
+        yr = ops.gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
+                      epilogue=L.EPI_BIAS | L.EPI_RESID)
+        aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        yg = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV), epilogue=L.EPI_BIAS | L.EPI_GELU,
+                      aux_out=aux)
+        ydg = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux)
+        p, seed = 0.25, 777
+        ydr = ops.gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
+                       epilogue=L.EPI_BIAS | L.EPI_DROPOUT | L.EPI_RESID, drop_seed=seed, drop_p=p)
+        acc0 = torch.randn(M, N, generator=g)
+        yac = acc0.clone().to(DEV)
+        ops.gemm(xd, wd, out=yac, epilogue=L.EPI_ACCUM, alpha=0.5)
+        torch.cuda.synchronize()
+    finally:
+        L.lib.cg_gemm_set_pers(old)
+    pre = base + bias
+    assert (y0.cpu() - base).abs().max() < tol
+    assert (y0b.float().cpu() - base).abs().max() < tol + 0.01 * base.abs().max()
+    assert (yb.float().cpu() - pre).abs().max() < tol + 0.01 * pre.abs().max()
+    assert (yr.cpu() - (pre + res)).abs().max() < tol
+    assert (aux.float().cpu() - pre).abs().max() < tol + 0.01 * pre.abs().max()
+    assert (yg.float().cpu() - F.gelu(pre)).abs().max() < tol + 0.01 * pre.abs().max()
+    xa = aux.float().cpu().requires_grad_(True)
+    F.gelu(xa).sum().backward()
+    assert (ydg.float().cpu() - base * xa.grad).abs().max() < tol + 0.01 * base.abs().max()
+    keep = torch.from_numpy(O.dropout_keep(seed, np.arange(M)[:, None], np.arange(N)[None, :], p))
+    ref = res + torch.where(keep, pre / (1 - p), torch.zeros(()))
+    assert (ydr.cpu() - ref).abs().max() < tol
+    assert (yac.cpu() - (acc0 + 0.5 * base)).abs().max() < tol
