@@ -51,16 +51,24 @@ __device__ __forceinline__ v8bf bfrag(const char* img, int wn, int j, int ks, in
 template <int EPI, int CT>
 struct Epi {
   static constexpr int W = CT == CG_BF16 ? 1 : 2;  // 16-B accesses per 8 values of C dtype
-  static constexpr int PER = W + ((EPI & CG_EPI_GELU) ? W : 0) + ((EPI & CG_EPI_DGELU) ? W : 0) +
-                             ((EPI & CG_EPI_RESID) ? 2 : 0) + ((EPI & CG_EPI_ACCUM) ? 2 : 0);
-  static constexpr int E = 8 * PER + ((EPI & CG_EPI_BIAS) ? 4 : 0);  // VMEM ops per wave per epilogue
+  // epilogue operand LOADS (bias, residual, dGELU pre-activation, accumulate source), issued
+  // at the top of the tile's last k-step, before that step's DMAs
+  static constexpr int L = 8 * (((EPI & CG_EPI_RESID) ? 2 : 0) + ((EPI & CG_EPI_DGELU) ? W : 0) +
+                                ((EPI & CG_EPI_ACCUM) ? 2 : 0)) + ((EPI & CG_EPI_BIAS) ? 4 : 0);
+  // epilogue STORES (C, GELU pre-activation), issued after the last k-step
+  static constexpr int S = 8 * (W + ((EPI & CG_EPI_GELU) ? W : 0));
 };
 
 __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
+// epilogue store cache policy: 0 = default.  (16 = sc1, which drops the written line from the
+// XCD's L2, measured no faster on the C4 shapes: the output stream is not what evicts operands.)
+#ifndef CG_STORE_CPOL
+#define CG_STORE_CPOL 0
+#endif
 __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, CG_STORE_CPOL);
 }
 __device__ __forceinline__ void unpack_f32(u32x4 a, u32x4 b, float v[8]) {
   v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
@@ -74,13 +82,14 @@ __device__ __forceinline__ void unpack_bf16(u32x4 a, float v[8]) {
     v[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
   }
 }
+typedef float v2f_t __attribute__((ext_vector_type(2)));
+typedef __bf16 v2bf_t __attribute__((ext_vector_type(2)));
+// one v_cvt_pk_bf16_f32 per pair (RNE, NaN kept)
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((v2f_t){a, b}, v2bf_t));
+}
 __device__ __forceinline__ u32x4 pack_bf16(const float v[8]) {
-  u32x4 u;
-  u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-  u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-  return u;
+  return (u32x4){pk2(v[0], v[1]), pk2(v[2], v[3]), pk2(v[4], v[5]), pk2(v[6], v[7])};
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
@@ -94,9 +103,9 @@ __device__ __forceinline__ void wait_vm() {
 template <int EPI, int CT>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
   using namespace bfp;
-  constexpr int E = Epi<EPI, CT>::E;
+  constexpr int NL = Epi<EPI, CT>::L, NS = Epi<EPI, CT>::S;
   constexpr int ES = CT == CG_BF16 ? 2 : 4;
-  static_assert(E + DMA_PER_STAGE <= 63, "vmcnt range");
+  static_assert(NL + NS + DMA_PER_STAGE <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
@@ -143,13 +152,72 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     for (int i = 0; i < B_CHUNKS; ++i) bfw::dma16(rb, st + A_BYTES + (wave + WAVES * i) * 1024, bo + vb[i]);
   };
 
+  // epilogue of local tile k straight from the accumulators: lane owns rows
+  // m0+wm+16i+(l&15) (i = 0..3) x columns n0+wn+32c+8(l>>4)+[0,8) (c = 0..1)
+  const __amdgpu_buffer_rsrc_t rc = rsrc(p.C, ((long long)(p.M - 1) * p.ldc + p.N) * ES);
+  const int g4 = lane >> 4, r16 = lane & 15;
+  u32x4 xa[4][2], xb[4][2], bq[2][2];
+  uint32_t off_c[4][2];
+  int col[2];
+  // operand loads of tile k (issued in its last k-step so that the compiler's wait for them in
+  // the epilogue does not also wait for the next tile's stage DMAs)
+  auto epi_loads = [&](int k) {
+    int m0, n0;
+    tile_org(k, m0, n0);
+    bool cok[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      col[c] = n0 + wn + 32 * c + 8 * g4;
+      cok[c] = col[c] < p.N;
+    }
+    if constexpr ((EPI & CG_EPI_BIAS) != 0) {
+      const __amdgpu_buffer_rsrc_t rbias = rsrc(p.bias, (long long)p.N * 4);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t o = cok[c] ? (uint32_t)col[c] * 4u : OOR;
+        bq[c][0] = bld(rbias, o);
+        bq[c][1] = bld(rbias, o + 16);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + wm + 16 * i + r16;
+      const bool rok = row < p.M;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bool ok = rok && cok[c];
+        off_c[i][c] = ok ? (uint32_t)(((long long)row * p.ldc + col[c]) * ES) : OOR;
+        if constexpr ((EPI & CG_EPI_RESID) != 0) {
+          const __amdgpu_buffer_rsrc_t rr = rsrc(p.resid, ((long long)(p.M - 1) * p.ldr + p.N) * 4);
+          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ldr + col[c]) * 4) : OOR;
+          xa[i][c] = bld(rr, o);
+          xb[i][c] = bld(rr, o + 16);
+        }
+        if constexpr ((EPI & CG_EPI_DGELU) != 0) {
+          const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux, ((long long)(p.M - 1) * p.ld_aux + p.N) * ES);
+          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ld_aux + col[c]) * ES) : OOR;
+          xa[i][c] = bld(rx, o);
+          if constexpr (CT != CG_BF16) xb[i][c] = bld(rx, o + 16);
+        }
+        if constexpr ((EPI & CG_EPI_ACCUM) != 0) {
+          xa[i][c] = bld(rc, off_c[i][c]);
+          xb[i][c] = bld(rc, off_c[i][c] + 16);
+        }
+      }
+    }
+  };
   v4f acc[4][4];
   // one k-step of global index g (the DMAs of stage g+2 interleaved with the MFMAs, as in the
   // non-persistent 256x128 kernel; they are always issued, so every step carries 6)
-  auto step = [&](int g, bool after_epi) {
-    if (after_epi) wait_vm<DMA_PER_STAGE + E>();
-    else wait_vm<DMA_PER_STAGE>();
+  // VMEM ops issued after stage g's DMAs, by position of step g in its tile (k = tile, t = step):
+  // stage g+1's DMAs always; the previous tile's epilogue stores when t < 2; its operand loads
+  // (issued in its last step, before that step's DMAs) when t == 0
+  auto step = [&](int g, int sel, auto last_tag) {
+    if (sel == 0) wait_vm<DMA_PER_STAGE>();
+    else if (sel == 1) wait_vm<DMA_PER_STAGE + NS>();
+    else wait_vm<DMA_PER_STAGE + NS + NL>();
     __builtin_amdgcn_s_barrier();
+    if constexpr (decltype(last_tag)::value) epi_loads(g / nt);
     const char* st = smem + (g % STAGES) * STAGE_BYTES;
     const char* as = st;
     const char* bs = st + A_BYTES;
@@ -187,57 +255,14 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
   };
 
-  // epilogue of local tile k straight from the accumulators: lane owns rows
-  // m0+wm+16i+(l&15) (i = 0..3) x columns n0+wn+32c+8(l>>4)+[0,8) (c = 0..1)
+  const bool scaled = p.alpha != 1.0f;
   auto epilogue = [&](int k) {
     int m0, n0;
     tile_org(k, m0, n0);
-    const int g4 = lane >> 4, r16 = lane & 15;
-    const __amdgpu_buffer_rsrc_t rc = rsrc(p.C, ((long long)(p.M - 1) * p.ldc + p.N) * ES);
-    int col[2];
-    bool cok[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      col[c] = n0 + wn + 32 * c + 8 * g4;
-      cok[c] = col[c] < p.N;
-    }
     float bia[2][8];
     if constexpr ((EPI & CG_EPI_BIAS) != 0) {
-      const __amdgpu_buffer_rsrc_t rbias = rsrc(p.bias, (long long)p.N * 4);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const uint32_t o = cok[c] ? (uint32_t)col[c] * 4u : OOR;
-        unpack_f32(bld(rbias, o), bld(rbias, o + 16), bia[c]);
-      }
-    }
-    // operand loads for the whole tile first (one wait for all of them)
-    u32x4 xa[4][2], xb[4][2];
-    uint32_t off_c[4][2];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + wm + 16 * i + r16;
-      const bool rok = row < p.M;
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const bool ok = rok && cok[c];
-        off_c[i][c] = ok ? (uint32_t)(((long long)row * p.ldc + col[c]) * ES) : OOR;
-        if constexpr ((EPI & CG_EPI_RESID) != 0) {
-          const __amdgpu_buffer_rsrc_t rr = rsrc(p.resid, ((long long)(p.M - 1) * p.ldr + p.N) * 4);
-          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ldr + col[c]) * 4) : OOR;
-          xa[i][c] = bld(rr, o);
-          xb[i][c] = bld(rr, o + 16);
-        }
-        if constexpr ((EPI & CG_EPI_DGELU) != 0) {
-          const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux, ((long long)(p.M - 1) * p.ld_aux + p.N) * ES);
-          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ld_aux + col[c]) * ES) : OOR;
-          xa[i][c] = bld(rx, o);
-          if constexpr (CT != CG_BF16) xb[i][c] = bld(rx, o + 16);
-        }
-        if constexpr ((EPI & CG_EPI_ACCUM) != 0) {
-          xa[i][c] = bld(rc, off_c[i][c]);
-          xb[i][c] = bld(rc, off_c[i][c] + 16);
-        }
-      }
+      for (int c = 0; c < 2; ++c) unpack_f32(bq[c][0], bq[c][1], bia[c]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -248,7 +273,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[4 * h + u] = acc[i][2 * c + h][u] * p.alpha;
+          for (int u = 0; u < 4; ++u) v[4 * h + u] = acc[i][2 * c + h][u];
+        if (scaled) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] *= p.alpha;
+        }
         if constexpr ((EPI & CG_EPI_BIAS) != 0) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += bia[c][j];
@@ -305,7 +334,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nt; ++t, ++g) step(g, k > 0 && t < 2);
+    for (int t = 0; t < nt - 1; ++t, ++g) step(g, k > 0 && t < 2 ? (t == 0 ? 2 : 1) : 0, std::false_type{});
+    step(g, k > 0 && nt - 1 < 2 ? 1 : 0, std::true_type{});  // nt >= 2: the last step is never t == 0
+    ++g;
     epilogue(k);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends

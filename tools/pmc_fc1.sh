@@ -1,0 +1,8 @@
+set -u
+mkdir -p gpurun_out/pmc_fc1
+cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+i=0
+for ctrs in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU"; do
+  i=$((i+1))
+  timeout -k 10 120 rocprofv3 --kernel-trace --pmc $ctrs -d gpurun_out/pmc_fc1/p$i -o run --output-format csv -- python tools/gemm_fc1_pmc.py > gpurun_out/pmc_fc1/p$i.log 2>&1 || exit 1
+done
