@@ -18,7 +18,7 @@ LIB_PATH = Path(os.environ.get("CG_LIB_PATH") or Path(__file__).resolve().parent
 
 CG_F32, CG_BF16 = 0, 1
 CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
-EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM = 1, 2, 4, 8, 16, 32
+EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1, 2, 4, 8, 16, 32, 64
 PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV = range(7)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
                PROBE_ATTN_FWD: "attn_fwd_mfma", PROBE_ATTN_DQ: "attn_bwd_dq_mfma",
@@ -102,6 +102,7 @@ SIGNATURES = {
     "cg_swiglu_bwd": (i32, [i32, vp, i64, i32, vp, i64, vp, i64, i32, i32, vp]),
     "cg_colsum_workspace": (sz, [i32, i32]),
     "cg_colsum": (i32, [i32, vp, i64, i32, i32, vp, i32, vp, vp]),
+    "cg_colsum_reduce": (i32, [vp, i32, i32, vp, i32, vp]),
     "cg_cast_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),

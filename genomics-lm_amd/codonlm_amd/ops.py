@@ -28,8 +28,9 @@ def _p(t):
 
 def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=None, out_dtype=None,
          bias=None, resid=None, epilogue=0, aux=None, aux_out=None, alpha=1.0, drop_seed=0, drop_p=0.0,
-         split_k=1):
-    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); A(m,k)=a[m,k] if a_kcontig else a[k,m]; same for B."""
+         split_k=1, colsum_out=None):
+    """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); A(m,k)=a[m,k] if a_kcontig else a[k,m]; same for B.
+    colsum_out (fp32 [N]): also the column sums of C (CG_EPI_COLSUM partials + cg_colsum_reduce)."""
     for t in (a, b):
         L.require_device(t, "gemm")
     if a.dtype != b.dtype:
@@ -46,6 +47,11 @@ def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=No
     ws = None
     if split_k > 1:
         ws = torch.empty(split_k * M * N, dtype=torch.float32, device=a.device)
+    if colsum_out is not None:
+        if split_k > 1:
+            raise ValueError("colsum_out needs split_k == 1")
+        epilogue = int(epilogue) | L.EPI_COLSUM
+        ws = torch.empty(((M + 63) // 64) * N, dtype=torch.float32, device=a.device)
     d = L.GemmDesc()
     d.in_dtype, d.c_dtype = _dt(a), _dt(out)
     d.M, d.N, d.K = M, N, K
@@ -63,6 +69,9 @@ def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=No
     d.drop_seed, d.drop_p = int(drop_seed) & 0xFFFFFFFF, float(drop_p)
     d.split_k, d.workspace = int(split_k), _p(ws)
     L.check(L.lib.cg_gemm(C.byref(d), L.stream_ptr(a.device)), "cg_gemm")
+    if colsum_out is not None:
+        L.check(L.lib.cg_colsum_reduce(ws.data_ptr(), (M + 63) // 64, N, colsum_out.data_ptr(), 0,
+                                       L.stream_ptr(a.device)), "cg_colsum_reduce")
     return out
 
 

@@ -198,6 +198,8 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,
                                         (long long)D.Vp * d, (long long)d * d});
   A.splitws_floats = (size_t)MAX_SPLIT * wmax;
+  // also holds the fused bias-gradient column-sum partials ([ceil(M/64)][cols])
+  A.splitws_floats = std::max<size_t>(A.splitws_floats, (size_t)((M + 63) / 64) * (size_t)big);
   A.splitws = w.take<float>(A.splitws_floats * 4);
   A.embws = w.take<float>((size_t)32 * D.V * d * 4);
   A.cews = w.take<float>((size_t)(1 + 256) * 4);
@@ -499,11 +501,13 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (!D.swiglu) {
       // (b2's gradient was produced by the LayerNorm backward that wrote gT)
       CK(lin_dw(C, A.gT, d, a.g, D.hid, d, D.hid, o.w2, D.hid, accumulate));
+      // dGELU product; its fused column sums (64-row partials) are fc1's bias gradient
       cg_gemm_desc g = lin_dx(C, A.gT, d, o.w2, D.hid, d, D.hid, A.dbig, D.hid, a.w2T);
-      g.epilogue = CG_EPI_DGELU; g.aux = a.a; g.ld_aux = D.hid;
+      g.epilogue = CG_EPI_DGELU | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
+      g.workspace = A.splitws;
       CK(cg_gemm(&g, C.s));
+      CK(cg_colsum_reduce(A.splitws, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
       CK(lin_dw(C, A.dbig, D.hid, a.h2, d, D.hid, d, o.w1, d, accumulate));
-      CK(bias_grad(C, A.dbig, D.hid, D.hid, o.b1, accumulate));
       g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dtmp, d, a.w1T);
       g.c_dtype = CG_F32;
       CK(cg_gemm(&g, C.s));

@@ -447,6 +447,18 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
 #include "gemm_wide.h"
 #include "gemm_pers.h"
 
+// CG_EPI_COLSUM fallback: part[r/64][n] = sum of C rows [64r, 64r+64) (column n)
+__global__ __launch_bounds__(256) void colsum64_kernel(const void* C, long long ldc, int ct, int M, int N,
+                                                       float* __restrict__ part) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const int r0 = blockIdx.y * 64, r1 = min(M, r0 + 64);
+  float acc = 0.f;
+  for (int r = r0; r < r1; ++r)
+    acc += ct == CG_BF16 ? bf2f(((const bf16_t*)C)[(long long)r * ldc + n]) : ((const float*)C)[(long long)r * ldc + n];
+  part[(long long)blockIdx.y * N + n] = acc;
+}
+
 // ---------------------------------------------------------------------------
 // host launcher
 // ---------------------------------------------------------------------------
@@ -501,6 +513,8 @@ static gemm_kernel_t pick_pers(int e, int ct) {
   PSPEC(CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
   PSPEC(CG_EPI_DGELU, CG_BF16)
   PSPEC(CG_EPI_ACCUM, CG_F32)
+  PSPEC(CG_EPI_DGELU | CG_EPI_COLSUM, CG_BF16)
+  PSPEC(CG_EPI_COLSUM, CG_BF16)
 #undef PSPEC
   return nullptr;
 }
@@ -596,6 +610,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   if ((p.epi & CG_EPI_RESID) && !p.resid) return CG_EINVAL;
   if ((p.epi & CG_EPI_GELU) && !p.aux_out) return CG_EINVAL;
   if ((p.epi & CG_EPI_DGELU) && !p.aux) return CG_EINVAL;
+  if ((p.epi & CG_EPI_COLSUM) && (!d->workspace || d->split_k > 1)) return CG_EINVAL;
   int split = d->split_k > 1 ? d->split_k : 1;
   const int bkt = d->in_dtype == CG_BF16 ? bfg::BKT : 16;
   if (d->K == 0) split = 1;
@@ -604,8 +619,11 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   if (split > 1 && !d->workspace) return CG_EINVAL;
   p.kchunk = kchunk; p.split = split; p.ws = d->workspace;
   bool vec = false;
+  const bool colsum = (p.epi & CG_EPI_COLSUM) != 0;
+  bool colsum_fused = false;
 
   if (d->in_dtype == CG_F32) {
+    p.epi &= ~CG_EPI_COLSUM;
     dim3 g(cg_cdiv(p.N, 64), cg_cdiv(p.M, 64), split);
     launch4(gemm_f32_kernel<false, false>, gemm_f32_kernel<false, true>, gemm_f32_kernel<true, false>,
             gemm_f32_kernel<true, true>, d->a_kcontig, d->b_kcontig, g, dim3(256), 0, s, p);
@@ -619,9 +637,12 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     size_t sh = bfg::SMEM;
     vec = vec_ok(d, split);
     gemm_kernel_t k;
+    const bool pers = vec && use_pers(d, split);
+    if (!pers) p.epi &= ~CG_EPI_COLSUM;  // only the persistent tile fuses the column sums
     const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
-    if (vec && use_pers(d, split)) {
+    if (pers) {
       k = pick_pers(p.epi, p.c_dtype);
+      colsum_fused = colsum;
       const int tiles = cg_cdiv(p.N, bfp::BN) * cg_cdiv(p.M, bfp::BM);
       g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cu_count()));
       blk = dim3(bfp::THREADS);
@@ -658,6 +679,11 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
       if (blocks > 4096) blocks = 4096;
       hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, p);
     }
+    CG_LAUNCH_CHECK();
+  }
+  if (colsum && !colsum_fused) {  // unfused fallback: the same 64-row partials, read back from C
+    hipLaunchKernelGGL(colsum64_kernel, dim3(cg_cdiv(p.N, 256), cg_cdiv(p.M, 64)), dim3(256), 0, s, p.C, p.ldc,
+                       p.c_dtype, p.M, p.N, p.ws);
     CG_LAUNCH_CHECK();
   }
   return CG_OK;

@@ -55,8 +55,8 @@ struct Epi {
   // at the top of the tile's last k-step, before that step's DMAs
   static constexpr int L = 8 * (((EPI & CG_EPI_RESID) ? 2 : 0) + ((EPI & CG_EPI_DGELU) ? W : 0) +
                                 ((EPI & CG_EPI_ACCUM) ? 2 : 0)) + ((EPI & CG_EPI_BIAS) ? 4 : 0);
-  // epilogue STORES (C, GELU pre-activation), issued after the last k-step
-  static constexpr int S = 8 * (W + ((EPI & CG_EPI_GELU) ? W : 0));
+  // epilogue STORES (C, GELU pre-activation, column-sum partials), issued after the last k-step
+  static constexpr int S = 8 * (W + ((EPI & CG_EPI_GELU) ? W : 0)) + ((EPI & CG_EPI_COLSUM) ? 4 : 0);
 };
 
 __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
@@ -264,6 +264,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) unpack_f32(bq[c][0], bq[c][1], bia[c]);
     }
+    float csum[2][8];
+    if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) csum[c][j] = 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + wm + 16 * i + r16;
@@ -316,12 +323,42 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += r[j];
         }
+        if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
+          const float keep = row < p.M ? 1.f : 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) csum[c][j] = fmaf(keep, v[j], csum[c][j]);
+        }
         if constexpr (CT == CG_BF16) {
           bst(rc, off_c[i][c], pack_bf16(v));
         } else {
           bst(rc, off_c[i][c], (u32x4){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
           bst(rc, off_c[i][c] + 16, (u32x4){__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
         }
+      }
+    }
+    if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
+      // sum over the 16 row lanes sharing these columns, then lane r16 == 0 writes the wave's
+      // 64-row partial (every lane issues the stores; the others at an out-of-range offset)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float t = csum[c][j];
+          t += __shfl_xor(t, 1, 64);
+          t += __shfl_xor(t, 2, 64);
+          t += __shfl_xor(t, 4, 64);
+          t += __shfl_xor(t, 8, 64);
+          csum[c][j] = t;
+        }
+      const int prow = (m0 + wm) >> 6;
+      const __amdgpu_buffer_rsrc_t rw = rsrc(p.ws, (long long)((p.M + 63) >> 6) * p.N * 4);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t o = (r16 == 0 && col[c] < p.N) ? (uint32_t)(((long long)prow * p.N + col[c]) * 4) : OOR;
+        bst(rw, o, (u32x4){__float_as_uint(csum[c][0]), __float_as_uint(csum[c][1]), __float_as_uint(csum[c][2]),
+                           __float_as_uint(csum[c][3])});
+        bst(rw, o + 16, (u32x4){__float_as_uint(csum[c][4]), __float_as_uint(csum[c][5]), __float_as_uint(csum[c][6]),
+                                __float_as_uint(csum[c][7])});
       }
     }
   };

@@ -137,6 +137,8 @@ extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, co
 }
 
 extern "C" int cg_layernorm_bwd_blocks(int rows) {
+  // 16 rows per block (4 per wave), at most 1024 blocks: measured faster than 32 rows/block
+  // (C4: 29.7 vs 38.2 us) although the dgamma/dbeta partial reduction then reads 2x more
   int b = cg_cdiv(rows, 16);
   return b > 1024 ? 1024 : (b < 1 ? 1 : b);
 }
@@ -703,13 +705,38 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const T_* __restrict__
   for (int r = r0; r < r1; ++r) s += ld_act<T_>(X + (long long)r * ldx + c);
   part[(long long)blockIdx.y * cols + c] = s;
 }
-__global__ void colsum_reduce_kernel(const float* __restrict__ part, int nch, int cols, float* __restrict__ out,
-                                     int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+// out[c] (+)= sum_i part[i][c]: 32 columns x 8 row lanes per block (fixed summation order)
+__global__ __launch_bounds__(256) void colsum_reduce_kernel(const float* __restrict__ part, int nch, int cols,
+                                                            float* __restrict__ out, int accumulate) {
+  __shared__ float red[8][33];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
   float s = 0.f;
-  for (int i = 0; i < nch; ++i) s += part[(long long)i * cols + c];
-  out[c] = accumulate ? out[c] + s : s;
+  if (c < cols) {   // four independent chains keep 4 loads in flight per lane
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    int i = rl;
+    for (; i + 24 < nch; i += 32)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += part[(long long)(i + 8 * u) * cols + c];
+    for (; i < nch; i += 8) s4[0] += part[(long long)i * cols + c];
+    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  }
+  red[rl][cl] = s;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += red[i][cl];
+    out[c] = accumulate ? out[c] + v : v;
+  }
+}
+extern "C" int cg_colsum_reduce(const float* part, int nparts, int cols, float* out, int accumulate, void* stream) {
+  if (cols <= 0) return CG_OK;
+  if (!part || !out || nparts < 0) return CG_EINVAL;
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 32)), dim3(256), 0, (hipStream_t)stream, part, nparts,
+                     cols, out, accumulate);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
 }
 // Fast path: 8 columns (one 16-B bf16 chunk / two float4) per thread, 32 column chunks x
 // 8 row lanes per 256-thread block, COLSUM_RB rows per block; partial rows reduced by
@@ -769,7 +796,7 @@ extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int 
     else
       hipLaunchKernelGGL(colsum_vec_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, (float*)ws);
     CG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 256)), dim3(256), 0, s, (const float*)ws, nrb, cols,
+    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 32)), dim3(256), 0, s, (const float*)ws, nrb, cols,
                        out, accumulate);
     CG_LAUNCH_CHECK();
     return CG_OK;
@@ -782,7 +809,7 @@ extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int 
   else
     hipLaunchKernelGGL(colsum_part_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, (float*)ws);
   CG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 256)), dim3(256), 0, s, (const float*)ws, nch, cols, out,
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 32)), dim3(256), 0, s, (const float*)ws, nch, cols, out,
                      accumulate);
   CG_LAUNCH_CHECK();
   return CG_OK;

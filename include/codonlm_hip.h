@@ -30,7 +30,10 @@ enum {
   CG_EPI_DGELU = 4,      /* out = v * gelu'(aux[m,n]) (aux in dtype of C)              */
   CG_EPI_RESID = 8,      /* out = resid[m,n] + v   (resid fp32, may alias C)           */
   CG_EPI_DROPOUT = 16,   /* v = v * keep(seed, m, n) / (1-p) before RESID              */
-  CG_EPI_ACCUM = 32      /* out (fp32) += v                                            */
+  CG_EPI_ACCUM = 32,     /* out (fp32) += v                                            */
+  CG_EPI_COLSUM = 64     /* also column sums of the final values into `workspace` as    */
+                         /* [ceil(M/64)][N] fp32 partials (reduce: cg_colsum_reduce) --  */
+                         /* a fused bias gradient; needs split_k == 1                     */
 };
 
 /*
@@ -140,6 +143,10 @@ int cg_swiglu_bwd(int dtype, const void* gu, long long ldgu, int Hp, const void*
 size_t cg_colsum_workspace(int rows, int cols);
 int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out,
               int accumulate, void* ws, void* stream);
+
+/* out[c] (+)= sum_i part[i*cols + c] over nparts partial rows (the second stage of the fused
+ * bias-gradient column sums, e.g. CG_EPI_COLSUM GEMM partials) */
+int cg_colsum_reduce(const float* part, int nparts, int cols, float* out, int accumulate, void* stream);
 
 /* batched transpose of 2-byte matrices: dst[c][r] = src[r][c]; rows, cols, lds, ldd multiples
  * of 8, 16-B aligned pointers.  Used to give the backward dX products K-contiguous weight

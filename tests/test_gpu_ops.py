@@ -306,6 +306,8 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K):
         acc0 = torch.randn(M, N, generator=g)
         yac = acc0.clone().to(DEV)
         ops.gemm(xd, wd, out=yac, epilogue=L.EPI_ACCUM, alpha=0.5)
+        cs = torch.empty(N, device=DEV)
+        ydc = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux, colsum_out=cs)
         torch.cuda.synchronize()
     finally:
         L.lib.cg_gemm_set_pers(old)
@@ -323,3 +325,29 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K):
     ref = res + torch.where(keep, pre / (1 - p), torch.zeros(()))
     assert (ydr.cpu() - ref).abs().max() < tol
     assert (yac.cpu() - (acc0 + 0.5 * base)).abs().max() < tol
+    ref_dg = base * xa.grad
+    assert (ydc.float().cpu() - ref_dg).abs().max() < tol + 0.01 * base.abs().max()
+    assert (cs.cpu() - ref_dg.sum(0)).abs().max() < 1e-2 * (1 + ref_dg.abs().sum(0).max())
+
+
+@pytest.mark.parametrize("dtype,pers", [(torch.float32, 1), (torch.bfloat16, 0), (torch.bfloat16, 1)])
+def test_gemm_colsum_epilogue(dtype, pers):
+    """CG_EPI_COLSUM (fused bias-gradient column sums) on the persistent tile and on the
+    unfused fallback (fp32 kernel / persistent tile disabled) against torch."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    M, N, K = 700, 264, 192
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * 0.1
+    base = (_bf(x) @ _bf(w).t()) if dtype == torch.bfloat16 else x @ w.t()
+    old = L.lib.cg_gemm_set_pers(pers)
+    try:
+        cs = torch.empty(N, device=DEV)
+        y = ops.gemm(x.to(DEV, dtype), w.to(DEV, dtype), out_dtype=dtype, colsum_out=cs)
+        torch.cuda.synchronize()
+    finally:
+        L.lib.cg_gemm_set_pers(old)
+    tol = 1e-3 if dtype == torch.float32 else 2e-2
+    assert (y.float().cpu() - base).abs().max() < tol * 4 * (1 + base.abs().max())
+    assert (cs.cpu() - base.sum(0)).abs().max() < tol * (1 + base.abs().sum(0).max())
