@@ -75,7 +75,9 @@ class Model(C.Structure):
                 ("loss_weights", vp), ("rope_cos", vp), ("rope_sin", vp),
                 ("workspace", vp), ("workspace_bytes", sz),
                 ("B", i32), ("T", i32), ("training", i32), ("window", i32), ("seed", u32),
-                ("idx", vp), ("targets", vp), ("logits", vp)]
+                ("idx", vp), ("targets", vp), ("logits", vp),
+                ("aux_ready", i32), ("head_grad_scale", f32), ("d_term_logits", vp), ("ld_d_term", i64),
+                ("d_offset_logits", vp * 8)]
 
 
 # name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
@@ -106,11 +108,15 @@ SIGNATURES = {
     "cg_cast_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),
+    "cg_cast_pad_2d": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp]),
+    "cg_offset_targets": (i32, [vp, i32, i32, i32, C.POINTER(i32), i32, vp, vp, vp]),
+    "cg_termination_labels": (i32, [vp, i32, i32, C.POINTER(i32), i32, C.POINTER(i32), i32, i32, vp, vp]),
     "cg_adamw": (i32, [vp, vp, vp, vp, vp, C.POINTER(AdamwSegment), i32, f32, f32, f32, i32, f32, vp]),
     "cg_nonfinite_flag": (i32, [vp, i64, vp, vp]),
     "cg_model_param_layout": (i32, [C.POINTER(ModelCfg), C.POINTER(ParamEntry), i32, C.POINTER(i64)]),
     "cg_model_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
     "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
+    "cg_model_aux_forward": (i32, [C.POINTER(Model), vp, i64, C.POINTER(vp), vp]),
     "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),
     "cg_model_hidden": (vp, [C.POINTER(Model), i32, C.POINTER(i32), C.POINTER(i64)]),
     "cg_probe_enable": (i32, [i32]),

@@ -186,6 +186,43 @@ class Engine:
                 "cg_model_forward")
         return logits, loss
 
+    def aux_forward(self):
+        """Aux heads of the last forward (model_tiny_gpt.py:329-337): termination logits
+        fp32 (M, n_classes) or None, and [offset logits fp32 (M, V)] in offset order."""
+        cfg = self.cfg
+        dev = self.flat.device
+        M = self.model.B * self.model.T
+        term = None
+        if cfg.termination_aux:
+            term = torch.empty(M, cfg.termination_n_classes, dtype=torch.float32, device=dev)
+        offs = [torch.empty(M, cfg.vocab_size, dtype=torch.float32, device=dev) for _ in cfg.multi_offset_targets]
+        arr = (C.c_void_p * len(offs))(*[o.data_ptr() for o in offs]) if offs else None
+        L.check(L.lib.cg_model_aux_forward(C.byref(self.model), term.data_ptr() if term is not None else None,
+                                           term.stride(0) if term is not None else 0, arr, L.stream_ptr(dev)),
+                "cg_model_aux_forward")
+        return term, offs
+
+    def set_head_grads(self, scale: float, d_term=None, d_offsets=None):
+        """Gradients phase 0 consumes: the next-codon loss scale and the aux-head logit
+        gradients (fp32, flattened to (M, cols)); None = that head is unused."""
+        m = self.model
+        m.head_grad_scale = float(scale)
+        keep = []
+        m.d_term_logits, m.ld_d_term = None, 0
+        if d_term is not None:
+            t = d_term.reshape(-1, d_term.shape[-1]).to(torch.float32).contiguous()
+            keep.append(t)
+            m.d_term_logits, m.ld_d_term = t.data_ptr(), t.stride(0)
+        for i in range(8):
+            m.d_offset_logits[i] = None
+        for i, g in enumerate(d_offsets or []):
+            if g is None:
+                continue
+            t = g.reshape(-1, g.shape[-1]).to(torch.float32).contiguous()
+            keep.append(t)
+            m.d_offset_logits[i] = t.data_ptr()
+        self._grad_keep = keep  # alive until the backward kernels are enqueued
+
     def backward_phase(self, phase: int, layer: int = 0, accumulate: bool = False):
         st = L.stream_ptr(self.flat.device)
         L.check(L.lib.cg_model_backward(C.byref(self.model), phase, layer, int(bool(accumulate)), st),

@@ -157,6 +157,31 @@ class _EngineBackward(torch.autograd.Function):
         return None, None, None
 
 
+class _AuxEngineBackward(torch.autograd.Function):
+    """Autograd node over (loss, termination logits, offset logits...) of a return_aux forward:
+    whatever objective the caller builds from them (objectives.py), its gradients w.r.t. these
+    outputs are handed to the native phase-0 backward in one call."""
+
+    @staticmethod
+    def forward(ctx, model, anchor, has_loss, has_term, *outs):
+        ctx.model, ctx.has_loss, ctx.has_term = model, has_loss, has_term
+        ctx.set_materialize_grads(False)  # unused heads arrive as None (their grads are zeroed)
+        if has_loss:
+            return (outs[0].clone(),) + tuple(outs[1:])
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        i = 0
+        g_loss = g_term = None
+        if ctx.has_loss:
+            g_loss, i = grads[0], 1
+        if ctx.has_term:
+            g_term, i = grads[i], i + 1
+        ctx.model._native_backward(g_loss, d_term=g_term, d_offsets=list(grads[i:]))
+        return (None, None, None, None) + (None,) * len(grads)
+
+
 class TinyGPT(nn.Module):
     def __init__(self, vocab_size, block_size, n_layer=3, n_head=4, n_embd=256, dropout=0.1, use_checkpoint=False,
                  label_smoothing: float = 0.0, sep_id: int | None = 3, tie_embeddings: bool = True,
@@ -356,14 +381,15 @@ class TinyGPT(nn.Module):
             mod, attr = self._param_by_name(name)
             getattr(mod, attr).grad = self._view(self._flat_grad, spec)
 
-    def _native_backward(self, gout):
-        scale = float(gout.detach().float().item())
+    def _native_backward(self, gout, d_term=None, d_offsets=None):
+        """Native backward of the last forward: ``gout`` = d(objective)/d(loss) (None when the
+        next-codon loss is unused), ``d_term`` / ``d_offsets`` = gradients of the aux logits."""
+        scale = 0.0 if gout is None else float(gout.detach().float().item())
         # an optimizer that set grads to None means "fresh group"
         if self.tok_emb.weight.grad is None:
             self._grads_fresh = True
-        if scale != 1.0:
-            raise NotImplementedError("backward of a scaled TinyGPT loss (scale the optimizer step instead)")
         eng = self.engine
+        eng.set_head_grads(scale, d_term, d_offsets)
         eng.backward(accumulate=not self._grads_fresh)
         self._grads_fresh = False
         self._bind_grad_views()
@@ -408,8 +434,7 @@ class TinyGPT(nn.Module):
         if shape_embeddings is not None:
             raise ValueError("shape guidance is not supported on the MI355X path")
         if return_aux and (self.termination_aux or self.multi_offset_targets):
-            from .aux_heads import aux_forward
-            return aux_forward(self, idx, targets, attention_window)
+            return self._forward_aux(idx, targets, attention_window)
         eng = self.engine
         training = self.training and self.dropout_p > 0
         seed = self.next_dropout_seed() if training else 0
@@ -419,6 +444,29 @@ class TinyGPT(nn.Module):
         if return_aux:
             return logits, loss, {}
         return logits, loss
+
+    def _forward_aux(self, idx, targets, attention_window):
+        """forward(..., return_aux=True) with aux heads: (logits, loss, {termination_logits,
+        offset_logits: {k: (B,T,V)}}) as model_tiny_gpt.py:326-351, all on the native engine."""
+        eng = self.engine
+        training = self.training and self.dropout_p > 0
+        seed = self.next_dropout_seed() if training else 0
+        logits, loss = eng.forward(idx, targets, training=training, seed=seed, window=attention_window)
+        term, offs = eng.aux_forward()
+        B, T = idx.shape
+        outs = ([loss] if loss is not None else []) + ([term.view(B, T, -1)] if term is not None else []) + \
+            [o.view(B, T, -1) for o in offs]
+        if self.training and torch.is_grad_enabled():
+            outs = list(_AuxEngineBackward.apply(self, self.tok_emb.weight, loss is not None, term is not None,
+                                                 *outs))
+        if loss is not None:
+            loss = outs.pop(0)
+        aux = {}
+        if term is not None:
+            aux["termination_logits"] = outs.pop(0)
+        if self.multi_offset_targets:
+            aux["offset_logits"] = {k: outs[i] for i, k in enumerate(self.multi_offset_targets)}
+        return logits, loss, aux
 
     @torch.no_grad()
     def iter_hidden_states(self, idx, shape_embeddings=None, attention_window: int | None = None):

@@ -170,6 +170,59 @@ def cast_to_bf16(x):
     return out.view(x.shape)
 
 
+def cast_pad_2d(src, dcols, dtype=torch.bfloat16):
+    """fp32 [rows][cols] -> dtype [rows][dcols], pad columns zero."""
+    L.require_device(src, "cast_pad_2d")
+    rows, cols = src.shape
+    out = torch.empty(rows, dcols, dtype=dtype, device=src.device)
+    L.check(L.lib.cg_cast_pad_2d(src.data_ptr(), src.stride(0), rows, cols, _dt(out), out.data_ptr(), out.stride(0),
+                                 dcols, L.stream_ptr(src.device)), "cg_cast_pad_2d")
+    return out
+
+
+def _ids(values):
+    vals = [int(v) for v in values]
+    return (C.c_int * max(1, len(vals)))(*vals), len(vals)
+
+
+def offset_targets(y, offset, boundary_ids=(2, 3), count=True):
+    """(targets, n_valid): y[:, t+k-1] where offset_target_mask is true, else PAD (0).
+    n_valid is a device int32 scalar (None with count=False)."""
+    L.require_device(y, "offset_targets")
+    y = y.to(torch.int64).contiguous()
+    B, T = y.shape
+    out = torch.empty_like(y)
+    nv = torch.zeros((), dtype=torch.int32, device=y.device) if count else None
+    ids, n = _ids(boundary_ids)
+    L.check(L.lib.cg_offset_targets(y.data_ptr(), B, T, int(offset), ids, n, out.data_ptr(), _p(nv),
+                                    L.stream_ptr(y.device)), "cg_offset_targets")
+    return out, nv
+
+
+def termination_labels(y, stop_ids, bucket_edges=(0, 3, 10, 30), ignore_index=-100):
+    L.require_device(y, "termination_labels")
+    y = y.to(torch.int64).contiguous()
+    B, T = y.shape
+    out = torch.empty_like(y)
+    st, ns = _ids(stop_ids)
+    ed, ne = _ids(bucket_edges)
+    L.check(L.lib.cg_termination_labels(y.data_ptr(), B, T, st, ns, ed, ne, int(ignore_index), out.data_ptr(),
+                                        L.stream_ptr(y.device)), "cg_termination_labels")
+    return out
+
+
+def colsum(x, out=None, accumulate=False):
+    """out[n] (+)= sum_m x[m, n] (fp32 out)."""
+    L.require_device(x, "colsum")
+    rows, cols = x.shape
+    if out is None:
+        out = torch.empty(cols, dtype=torch.float32, device=x.device)
+    ws = torch.empty(int(L.lib.cg_colsum_workspace(rows, cols)) // 4 + 1, dtype=torch.float32, device=x.device)
+    L.check(L.lib.cg_colsum(_dt(x), x.data_ptr(), x.stride(0), rows, cols, out.data_ptr(), int(bool(accumulate)),
+                            ws.data_ptr(), L.stream_ptr(x.device)), "cg_colsum")
+    return out
+
+
 def transpose16(mats):
     """Batched transpose of 2-byte 2-D tensors (one launch); returns the contiguous transposes."""
     if len(mats) > L.TRANSPOSE_MAX:

@@ -104,7 +104,8 @@ void build_layout(const cg_model_cfg* c, const Dims& D, Layout& Lo) {
   if (!c->tie_embeddings) Lo.head = add(CG_P_HEAD_W, -1, D.V, d, d, (long long)D.Vp * d, true);
   if (c->termination_aux) {
     const int nc = c->termination_n_classes;
-    Lo.termw = add(CG_P_TERM_W, -1, nc, d, d, (long long)nc * d, true);
+    // rows padded to 16 (zero) so the backward products see an extent the bf16 tiles take
+    Lo.termw = add(CG_P_TERM_W, -1, nc, d, d, rup(nc, 16) * d, true);
     Lo.termb = add(CG_P_TERM_B, -1, nc, 0, nc, nc, true);
   }
   for (int i = 0; i < c->n_offsets && i < 8; ++i) {
@@ -148,6 +149,8 @@ struct Acts {
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
   size_t splitws_floats;
   bool wT;  // transposed weight copies present
+  // auxiliary offset heads: pre-GELU a, GELU output g, projection pj (compute dtype, M x d)
+  std::vector<void*> oa, og, opj;
 };
 
 constexpr int MAX_SPLIT = 8;
@@ -184,6 +187,13 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.rstdf = w.take<float>(M * 4);
   A.xf = w.take<char>(M * d * es);
   A.logits_int = w.take<float>(M * D.V * 4);
+  const int noff = std::min(c->n_offsets, 8);
+  A.oa.assign(noff, nullptr); A.og.assign(noff, nullptr); A.opj.assign(noff, nullptr);
+  for (int i = 0; i < noff; ++i) {
+    A.oa[i] = w.take<char>(M * d * es);
+    A.og[i] = w.take<char>(M * d * es);
+    A.opj[i] = w.take<char>(M * d * es);
+  }
   A.dlogits = w.take<char>(M * D.Vp * es);
   A.gT = w.take<char>(M * d * es);
   const long long big = std::max<long long>({(long long)D.hid, 2LL * D.Hp, (long long)D.Nqkv});
@@ -356,6 +366,93 @@ int bias_grad(const Ctx& C, const void* dy, long long lddy, int N, long long gof
 
 float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 
+int zero_grad(const Ctx& C, long long off, long long elems) {
+  return hipMemsetAsync(G(C, off), 0, (size_t)elems * 4, C.s) == hipSuccess ? CG_OK : CG_ELAUNCH;
+}
+
+// Backward of the auxiliary heads (model_tiny_gpt.py:329-337) inside phase 0: parameter grads
+// of termination_head / offset_projs, the tied head's extra gradient, and their share of dxf
+// (added into A.dtmp before the ln_f backward).  A.dlogits is free here (head products done).
+int aux_backward(const Ctx& C, int accumulate) {
+  const cg_model* m = C.m;
+  const Dims& D = C.D;
+  const Acts& A = C.A;
+  const int d = D.d;
+  const long long M = C.M;
+  const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+  if (m->cfg.termination_aux) {
+    const int nc = m->cfg.termination_n_classes, ncp = (int)rup(nc, 16);
+    if (m->d_term_logits) {
+      if (!m->aux_ready || m->ld_d_term < nc) return CG_EINVAL;
+      CK(cg_cast_pad_2d(m->d_term_logits, m->ld_d_term, (int)M, nc, C.dt, A.dlogits, ncp, ncp, C.s));
+      // dW_t = dT^T . xf over the padded rows (pad rows of dT^T are zero)
+      cg_gemm_desc g = gdesc(C);
+      g.c_dtype = CG_F32;
+      g.M = ncp; g.N = d; g.K = (int)M;
+      g.A = A.dlogits; g.lda = ncp; g.a_kcontig = 0;
+      g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
+      g.C = G(C, C.Lo.termw); g.ldc = d;
+      g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
+      g.split_k = pick_split(C, ncp, d, M);
+      g.workspace = A.splitws;
+      CK(cg_gemm(&g, C.s));
+      CK(cg_colsum(CG_F32, m->d_term_logits, m->ld_d_term, (int)M, nc, G(C, C.Lo.termb), accumulate, A.colws,
+                   C.s));
+      // dxf += dT . W_t
+      g = lin_dx(C, A.dlogits, ncp, C.Lo.termw, d, ncp, d, A.dtmp, d);
+      g.c_dtype = CG_F32;
+      g.epilogue = CG_EPI_RESID; g.resid = A.dtmp; g.ldr = d;
+      CK(cg_gemm(&g, C.s));
+    } else if (!accumulate) {
+      CK(zero_grad(C, C.Lo.termw, (long long)ncp * d));
+      CK(zero_grad(C, C.Lo.termb, nc));
+    }
+  }
+  const int noff = std::min(m->cfg.n_offsets, 8);
+  for (int i = 0; i < noff; ++i) {
+    const float* dl = m->d_offset_logits[i];
+    if (!dl) {
+      if (!accumulate) {
+        CK(zero_grad(C, C.Lo.off1w[i], (long long)d * d));
+        CK(zero_grad(C, C.Lo.off1b[i], d));
+        CK(zero_grad(C, C.Lo.off2w[i], (long long)d * d));
+        CK(zero_grad(C, C.Lo.off2b[i], d));
+      }
+      continue;
+    }
+    if (!m->aux_ready) return CG_EINVAL;
+    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt, A.dlogits, D.Vp, D.Vp, C.s));
+    // d(head) += Gc^T . pj   (phase 0's own head product initialised it)
+    cg_gemm_desc g = gdesc(C);
+    g.c_dtype = CG_F32;
+    g.M = D.Vp; g.N = d; g.K = (int)M;
+    g.A = A.dlogits; g.lda = D.Vp; g.a_kcontig = 0;
+    g.B = A.opj[i]; g.ldb = d; g.b_kcontig = 0;
+    g.C = G(C, hoff); g.ldc = d;
+    g.epilogue = CG_EPI_ACCUM;
+    g.split_k = pick_split(C, D.Vp, d, M);
+    g.workspace = A.splitws;
+    CK(cg_gemm(&g, C.s));
+    // dpj = Gc . E ; the second Linear's grads
+    g = lin_dx(C, A.dlogits, D.Vp, hoff, d, D.Vp, d, A.dsmall, d);
+    CK(cg_gemm(&g, C.s));
+    CK(lin_dw(C, A.dsmall, d, A.og[i], d, d, d, C.Lo.off2w[i], d, accumulate));
+    CK(bias_grad(C, A.dsmall, d, d, C.Lo.off2b[i], accumulate));
+    // da = (dpj . W2) * gelu'(a) ; the first Linear's grads
+    g = lin_dx(C, A.dsmall, d, C.Lo.off2w[i], d, d, d, A.dbig, d);
+    g.epilogue = CG_EPI_DGELU; g.aux = A.oa[i]; g.ld_aux = d;
+    CK(cg_gemm(&g, C.s));
+    CK(lin_dw(C, A.dbig, d, A.xf, d, d, d, C.Lo.off1w[i], d, accumulate));
+    CK(bias_grad(C, A.dbig, d, d, C.Lo.off1b[i], accumulate));
+    // dxf += da . W1
+    g = lin_dx(C, A.dbig, d, C.Lo.off1w[i], d, d, d, A.dtmp, d);
+    g.c_dtype = CG_F32;
+    g.epilogue = CG_EPI_RESID; g.resid = A.dtmp; g.ldr = d;
+    CK(cg_gemm(&g, C.s));
+  }
+  return CG_OK;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -386,6 +483,9 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   if (m->cfg.use_rope && (!m->rope_cos || !m->rope_sin)) return CG_EINVAL;
   m->B = B; m->T = T; m->training = training; m->seed = seed; m->window = window;
   m->idx = idx; m->targets = targets;
+  m->aux_ready = 0; m->head_grad_scale = 1.0f;
+  m->d_term_logits = nullptr; m->ld_d_term = 0;
+  for (int i = 0; i < 8; ++i) m->d_offset_logits[i] = nullptr;
   Ctx C;
   CK(make_ctx(m, B, T, stream, C));
   const Dims& D = C.D;
@@ -451,9 +551,46 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   return CG_OK;
 }
 
+extern "C" int cg_model_aux_forward(cg_model* m, float* term_logits, long long ld_term, float* const* offset_logits,
+                                    void* stream) {
+  if (!m || !m->idx || m->B <= 0 || m->T <= 0) return CG_EINVAL;
+  const int nc = m->cfg.termination_aux ? m->cfg.termination_n_classes : 0;
+  const int noff = std::min(m->cfg.n_offsets, 8);
+  if (nc > 0 && (!term_logits || ld_term < nc)) return CG_EINVAL;
+  if (noff > 0 && !offset_logits) return CG_EINVAL;
+  for (int i = 0; i < noff; ++i)
+    if (!offset_logits[i]) return CG_EINVAL;
+  Ctx C;
+  CK(make_ctx(m, m->B, m->T, stream, C));
+  const Dims& D = C.D;
+  const Acts& A = C.A;
+  const int d = D.d;
+  if (nc > 0) {
+    cg_gemm_desc g = lin_fwd(C, A.xf, d, C.Lo.termw, d, nc, d, term_logits, ld_term);
+    g.c_dtype = CG_F32;
+    g.epilogue = CG_EPI_BIAS; g.bias = P(C, C.Lo.termb);
+    CK(cg_gemm(&g, C.s));
+  }
+  const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+  for (int i = 0; i < noff; ++i) {
+    // offset_projs[k] = Linear -> GELU -> Linear, then the (tied) head
+    cg_gemm_desc g = lin_fwd(C, A.xf, d, C.Lo.off1w[i], d, d, d, A.og[i], d);
+    g.epilogue = CG_EPI_BIAS | CG_EPI_GELU; g.bias = P(C, C.Lo.off1b[i]);
+    g.aux_out = A.oa[i]; g.ld_aux = d;
+    CK(cg_gemm(&g, C.s));
+    g = lin_fwd(C, A.og[i], d, C.Lo.off2w[i], d, d, d, A.opj[i], d);
+    g.epilogue = CG_EPI_BIAS; g.bias = P(C, C.Lo.off2b[i]);
+    CK(cg_gemm(&g, C.s));
+    g = lin_fwd(C, A.opj[i], d, hoff, d, D.V, d, offset_logits[i], D.V);
+    g.c_dtype = CG_F32;
+    CK(cg_gemm(&g, C.s));
+  }
+  m->aux_ready = 1;
+  return CG_OK;
+}
+
 extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* stream) {
   if (!m || !m->idx || !m->grads) return CG_EINVAL;
-  if (!m->targets) return CG_EINVAL;
   Ctx C;
   CK(make_ctx(m, m->B, m->T, stream, C));
   const Dims& D = C.D;
@@ -467,21 +604,31 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   if (phase == 0) {
     CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
-    // d(head weight) = dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero)
-    cg_gemm_desc g = gdesc(C);
-    g.c_dtype = CG_F32;
-    g.M = D.Vp; g.N = d; g.K = (int)M;
-    g.A = A.dlogits; g.lda = D.Vp; g.a_kcontig = 0;
-    g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
-    g.C = G(C, hoff); g.ldc = d;
-    g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
-    g.split_k = pick_split(C, D.Vp, d, M);
-    g.workspace = A.splitws;
-    CK(cg_gemm(&g, C.s));
-    // dxf = dlogits . E
-    g = lin_dx(C, A.dlogits, D.Vp, hoff, d, D.Vp, d, A.dtmp, d);
-    g.c_dtype = CG_F32;
-    CK(cg_gemm(&g, C.s));
+    if (m->targets) {
+      // d(head weight) = s dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero)
+      cg_gemm_desc g = gdesc(C);
+      g.c_dtype = CG_F32;
+      g.M = D.Vp; g.N = d; g.K = (int)M;
+      g.A = A.dlogits; g.lda = D.Vp; g.a_kcontig = 0;
+      g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
+      g.C = G(C, hoff); g.ldc = d;
+      g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
+      g.alpha = m->head_grad_scale;
+      g.split_k = pick_split(C, D.Vp, d, M);
+      g.workspace = A.splitws;
+      CK(cg_gemm(&g, C.s));
+      // dxf = s dlogits . E
+      g = lin_dx(C, A.dlogits, D.Vp, hoff, d, D.Vp, d, A.dtmp, d);
+      g.c_dtype = CG_F32;
+      g.alpha = m->head_grad_scale;
+      CK(cg_gemm(&g, C.s));
+    } else {
+      // no next-codon loss (aux-only objective, e.g. a replay batch): nothing to scale
+      if (m->head_grad_scale != 0.f || !m->aux_ready) return CG_EINVAL;
+      if (!accumulate) CK(zero_grad(C, hoff, (long long)D.Vp * d));
+      if (hipMemsetAsync(A.dtmp, 0, (size_t)M * d * 4, C.s) != hipSuccess) return CG_ELAUNCH;
+    }
+    CK(aux_backward(C, accumulate));  // aux heads add into d(head) and dxf
     float* xL = A.x + (size_t)D.L * M * d;
     const int ll = D.L - 1;
     // gT feeds block L-1's MLP output Linear: its bias gradient (GELU mode) is gT's column sum

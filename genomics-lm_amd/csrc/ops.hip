@@ -1022,6 +1022,144 @@ extern "C" int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n,
   return CG_OK;
 }
 
+// fp32 [rows][cols] -> dtype [rows][dcols] with zero pad columns (aux-head logit grads into
+// the padded GEMM operand layout)
+template <typename T_>
+__global__ __launch_bounds__(256) void cast_pad_kernel(const float* __restrict__ src, long long lds, int rows, int cols,
+                                                       T_* __restrict__ dst, long long ldd, int dcols) {
+  const long long total = (long long)rows * dcols;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long r = i / dcols;
+    const int c = (int)(i - r * dcols);
+    st_act<T_>(dst + r * ldd + c, c < cols ? src[r * lds + c] : 0.f);
+  }
+}
+extern "C" int cg_cast_pad_2d(const float* src, long long lds, int rows, int cols, int dtype, void* dst, long long ldd,
+                              int dcols, void* stream) {
+  if (rows < 0 || cols < 0 || dcols < cols || lds < cols || ldd < dcols) return CG_EINVAL;
+  const long long total = (long long)rows * dcols;
+  if (total == 0) return CG_OK;
+  if (!src || !dst) return CG_EINVAL;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 8192) blocks = 8192;
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(cast_pad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, lds, rows, cols,
+                       (bf16_t*)dst, ldd, dcols);
+  else if (dtype == CG_F32)
+    hipLaunchKernelGGL(cast_pad_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, lds, rows, cols,
+                       (float*)dst, ldd, dcols);
+  else
+    return CG_EUNSUPPORTED;
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
+// Auxiliary objectives' labels (src/codonlm/training/objectives.py): integer work, one
+// thread per (b, t), ids passed by value.
+// ===========================================================================
+struct IdSet {
+  int n;
+  int id[8];
+};
+__device__ __forceinline__ bool in_set(const IdSet& s, int64_t v) {
+  bool r = false;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r |= (i < s.n) && (v == (int64_t)s.id[i]);
+  return r;
+}
+static bool make_set(const int* ids, int n, IdSet& s) {
+  if (n < 0 || n > 8 || (n > 0 && !ids)) return false;
+  s.n = n;
+  for (int i = 0; i < 8; ++i) s.id[i] = i < n ? ids[i] : 0;
+  return true;
+}
+// offset_target_mask (objectives.py:6-23): target y[t+k-1] is valid when it exists, is not PAD
+// and no boundary id occurs in y[t .. t+k-2]; invalid targets become PAD (ignored by the CE)
+__global__ __launch_bounds__(256) void offset_targets_kernel(const int64_t* __restrict__ y, int B, int T, int k,
+                                                             IdSet bnd, int64_t* __restrict__ out,
+                                                             int* __restrict__ nvalid) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  int v = 0;
+  if (i < (long long)B * T) {
+    const long long b = i / T;
+    const int t = (int)(i - b * T);
+    const int64_t* row = y + b * T;
+    int64_t tgt = 0;
+    if (t + k - 1 < T) {
+      tgt = row[t + k - 1];
+      bool ok = tgt != 0;
+      for (int s = 0; s < k - 1 && ok; ++s) ok = !in_set(bnd, row[t + s]);
+      if (!ok) tgt = 0;
+    }
+    out[i] = tgt;
+    v = tgt != 0;
+  }
+  if (nvalid) {  // uniform branch: every lane reaches the ballot
+    const unsigned long long bal = __ballot(v);
+    if ((threadIdx.x & 63) == 0 && bal) atomicAdd(nvalid, (int)__popcll(bal));
+  }
+}
+extern "C" int cg_offset_targets(const int64_t* y, int B, int T, int offset, const int* boundary_ids, int n_boundary,
+                                 int64_t* out, int* n_valid, void* stream) {
+  IdSet bnd;
+  if (B < 0 || T < 0 || offset < 1 || !make_set(boundary_ids, n_boundary, bnd)) return CG_EINVAL;
+  const long long total = (long long)B * T;
+  if (total == 0) return CG_OK;
+  if (!y || !out) return CG_EINVAL;
+  hipLaunchKernelGGL(offset_targets_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y,
+                     B, T, offset, bnd, out, n_valid);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+// termination_distance_bucket_labels (objectives.py:63-91): distance to the next stop id at or
+// after t, bucketed as #(edges < distance); no later stop -> n_edges; PAD -> ignore_index
+__global__ __launch_bounds__(256) void termination_labels_kernel(const int64_t* __restrict__ y, int B, int T,
+                                                                 IdSet stops, IdSet edges, int ignore,
+                                                                 int64_t* __restrict__ lab) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * T) return;
+  const long long b = i / T;
+  const int t = (int)(i - b * T);
+  const int64_t* row = y + b * T;
+  int64_t out;
+  if (row[t] == 0) {
+    out = ignore;
+  } else {
+    int nxt = T;
+    for (int s = t; s < T; ++s)
+      if (in_set(stops, row[s])) {
+        nxt = s;
+        break;
+      }
+    if (nxt == T) {
+      out = edges.n;
+    } else {
+      const int dist = nxt - t;
+      int c = 0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) c += (e < edges.n) && (dist > edges.id[e]);
+      out = c;
+    }
+  }
+  lab[i] = out;
+}
+extern "C" int cg_termination_labels(const int64_t* y, int B, int T, const int* stop_ids, int n_stop, const int* edges,
+                                     int n_edges, int ignore_index, int64_t* labels, void* stream) {
+  IdSet st, ed;
+  if (B < 0 || T < 0 || n_stop < 1 || !make_set(stop_ids, n_stop, st) || !make_set(edges, n_edges, ed))
+    return CG_EINVAL;
+  for (int e = 1; e < n_edges; ++e)
+    if (edges[e] < edges[e - 1]) return CG_EINVAL;
+  const long long total = (long long)B * T;
+  if (total == 0) return CG_OK;
+  if (!y || !labels) return CG_EINVAL;
+  hipLaunchKernelGGL(termination_labels_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, y, B, T, st, ed, ignore_index, labels);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
 // ===========================================================================
 // Batched 2-byte transpose (bf16 weight matrices -> K-contiguous operands for the
 // backward dX products, so they run on the LDS-DMA tile).  64x64 tiles through LDS,

@@ -166,6 +166,21 @@ int cg_transpose16_batch(const cg_transpose_batch* tb, void* stream);
 /* elementwise casts / utilities */
 int cg_cast_f32_to_bf16(const float* src, uint16_t* dst, long long n, void* stream);
 int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stream);
+/* dst[r][c] = src[r][c] (c < cols), 0 for cols <= c < dcols; dst in `dtype` */
+int cg_cast_pad_2d(const float* src, long long lds, int rows, int cols, int dtype, void* dst,
+                   long long ldd, int dcols, void* stream);
+
+/* Auxiliary objectives' label construction (src/codonlm/training/objectives.py).
+ * offset targets (offset_target_mask :6-23): out[b][t] = y[b][t+k-1] where that target is
+ * valid (t+k-1 < T, not PAD, no boundary id among y[b][t..t+k-2]), else 0 (= ignored by the
+ * PAD-ignoring cross-entropy); *n_valid (device int, optional) += number of valid targets. */
+int cg_offset_targets(const int64_t* y, int B, int T, int offset, const int* boundary_ids,
+                      int n_boundary, int64_t* out, int* n_valid, void* stream);
+/* termination_distance_bucket_labels (:63-91): distance to the next stop id bucketed by
+ * the sorted edges (count of edges < distance); no later stop -> n_edges; PAD -> ignore. */
+int cg_termination_labels(const int64_t* y, int B, int T, const int* stop_ids, int n_stop,
+                          const int* edges, int n_edges, int ignore_index, int64_t* labels,
+                          void* stream);
 
 /* Fused AdamW over the flat parameter buffer (torch.optim.AdamW semantics,
  * loop.py:681-731): up to 4 contiguous segments with their own (lr, wd); grads are
@@ -227,6 +242,14 @@ typedef struct {
   const int64_t* idx;
   const int64_t* targets;
   float* logits;
+  /* auxiliary heads (model_tiny_gpt.py:329-337).  cg_model_forward resets these to
+   * (0, 1, NULL...); the caller sets the gradients of the aux outputs between
+   * cg_model_aux_forward and cg_model_backward phase 0. */
+  int aux_ready;                    /* set by cg_model_aux_forward                      */
+  float head_grad_scale;            /* d(objective)/d(next-codon loss)                  */
+  const float* d_term_logits;       /* fp32 [B*T][ld_d_term] or NULL                    */
+  long long ld_d_term;
+  const float* d_offset_logits[8];  /* fp32 [B*T][V] per offset head, or NULL           */
 } cg_model;
 
 /* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
@@ -235,8 +258,17 @@ typedef struct {
 int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, int B, int T,
                      int training, uint32_t seed, int window, float* logits, float* loss,
                      void* stream);
+/* auxiliary heads on the ln_f output of the last forward (model_tiny_gpt.py:329-337):
+ * termination logits fp32 [B*T][ld_term] = xf W_t^T + b_t (termination_aux), and per
+ * offset head i: logits_i fp32 [B*T][V] = head(W2 gelu(W1 xf + b1) + b2) (tied head).
+ * The offset activations stay in the workspace for the backward. */
+int cg_model_aux_forward(cg_model* m, float* term_logits, long long ld_term,
+                         float* const* offset_logits, void* stream);
 /* backward in phases so the caller can overlap per-bucket gradient all-reduce:
- *   phase 0: head + ln_f; phase 1: one block `layer` (call L-1 .. 0); phase 2: embeddings.
+ *   phase 0: head (+ aux heads) + ln_f; phase 1: one block `layer` (call L-1 .. 0);
+ *   phase 2: embeddings.  Phase 0 scales the next-codon head gradient by head_grad_scale
+ *   and adds the aux-head gradients given in d_term_logits / d_offset_logits; aux
+ *   parameters without a gradient are zeroed when accumulate=0.
  * accumulate=0 overwrites grads (first microbatch of a group), 1 adds. */
 int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* stream);
 /* pointer to hidden state `which` (0 = embedding output, 1..L = block outputs,

@@ -21,6 +21,8 @@ follows (paths relative to the upstream repo AvishaiBarnoy/genomics-lm):
 * ``lr_lambda``          src/codonlm/training/loop.py:770-779
 * ``offset_target_mask`` / ``termination_labels``
                          src/codonlm/training/objectives.py:6-23, 63-91
+* ``multi_offset_loss`` / ``termination_loss`` / ``objective_backward``
+                         objectives.py:26-60, 94-105; loop.py:1075-1112
 * ``pool_state``         scripts/extract_embeddings.py:94-114
 
 Parity pinning: the restatement is checked against golden vectors produced by
@@ -475,6 +477,62 @@ def termination_labels(yb, stop_ids, bucket_edges=(0, 3, 10, 30), ignore_index=-
                 dist = nxt - t
                 out[b, t] = sum(1 for e in bucket_edges if dist > e)
     return out
+
+
+def multi_offset_loss(offset_logits: dict, yb, offset_weights: dict, eps=0.0, loss_weights=None,
+                      boundary_ids=(2, 3)):
+    """multi_offset_lm_loss restated (objectives.py:26-60): CE on the gathered valid rows."""
+    yb = torch.as_tensor(np.asarray(yb), dtype=torch.long)
+    T = yb.shape[1]
+    total = torch.zeros(())
+    losses = {}
+    for k, w in offset_weights.items():
+        if w == 0.0 or k <= 1 or k > T or k not in offset_logits:
+            continue
+        valid = offset_target_mask(yb, k, boundary_ids)
+        if not bool(valid.any()):
+            continue
+        pred = offset_logits[k][:, : T - k + 1][valid]
+        tgt = yb[:, k - 1:][valid]
+        lk = cross_entropy(pred, tgt, eps, loss_weights)
+        losses[k] = lk
+        total = total + float(w) * lk
+    return total, losses
+
+
+def termination_loss(term_logits, labels, class_weights=None, ignore_index=-100):
+    """termination_aux_loss restated (objectives.py:94-105)."""
+    nc = term_logits.shape[-1]
+    lab = torch.as_tensor(np.asarray(labels), dtype=torch.long).reshape(-1)
+    return cross_entropy(term_logits.reshape(-1, nc), lab, 0.0, class_weights, ignore_index)
+
+
+def objective_backward(cfg, params, idx, targets, offset_weights, term_weight, stop_ids,
+                       bucket_edges=(0, 3, 10, 30), term_class_weights=None):
+    """The trainer's objective with aux heads (loop.py:1075-1112) and its parameter grads."""
+    P = _to_t(params, True)
+    o = forward(cfg, P, idx, targets)
+    total = o["loss"]
+    lw = None
+    if cfg.loss_weights is not None and not all(float(v) == 1.0 for v in cfg.loss_weights):
+        lw = torch.tensor(cfg.loss_weights, dtype=torch.float32)
+    parts = {"loss": o["loss"], "aux": o["aux"]}
+    if cfg.multi_offset_targets:
+        off_total, off_losses = multi_offset_loss(o["aux"]["offset_logits"], targets, offset_weights,
+                                                  cfg.label_smoothing, lw)
+        total = total + off_total
+        parts.update({f"offset_loss_{k}": v for k, v in off_losses.items()})
+    if cfg.termination_aux:
+        labels = termination_labels(targets, tuple(stop_ids), tuple(bucket_edges))
+        cw = None if term_class_weights is None else torch.tensor(term_class_weights, dtype=torch.float32)
+        tl = termination_loss(o["aux"]["termination_logits"], labels, cw)
+        total = total + term_weight * tl
+        parts["term_loss"] = tl
+        parts["term_labels"] = labels
+    total.backward()
+    grads = {k: (v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v)) for k, v in P.items()}
+    parts["total"] = total
+    return parts, grads
 
 
 def pool_state(hidden, idx, mode, content_ids, pad=PAD_ID):

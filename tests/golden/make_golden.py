@@ -208,8 +208,60 @@ def objectives_case():
     print("[golden] objectives")
 
 
+AUX_OBJECTIVE = dict(offset_weights={2: 0.5, 4: 0.25}, term_weight=0.1, stop_ids=(2, 52),
+                     bucket_edges=(0, 3, 10, 30), term_class_weights=[1.0, 2.0, 1.5, 1.0, 0.5])
+
+
+def aux_objective_case():
+    """The codon trainer's full objective with aux heads (loop.py:1075-1112): next-codon CE +
+    multi_offset_lm_loss + w_t * termination_aux_loss, backpropagated through the reference
+    TinyGPT; all parameter grads (incl. offset_projs / termination_head) are stored."""
+    cfg = OracleConfig(vocab_size=68, block_size=64, n_layer=1, n_head=4, n_embd=64, sep_id=3,
+                       label_smoothing=0.05, termination_aux=True, multi_offset_targets=[2, 4],
+                       loss_weights=[1.0, 1.0, 3.0] + [1.0] * 65)
+    rng = np.random.default_rng(4321)
+    params = synthetic_params(cfg, seed=77)
+    idx, tgt = packed_tokens(rng, 2, 64, pad_tail=6, sep_every=14)
+    tgt[0, 20] = 52  # a stop codon id inside a segment
+    model = build_ref(cfg, params)
+    model.train()  # dropout=0: train mode only matters for the trainer path
+    x, y = torch.from_numpy(idx), torch.from_numpy(tgt)
+    A = AUX_OBJECTIVE
+    logits, loss, aux = model(x, y, return_aux=True)
+    lw = model.loss_weights if not torch.all(model.loss_weights == 1.0).item() else None
+    off_total, off_losses = ref_obj.multi_offset_lm_loss(aux["offset_logits"], y, A["offset_weights"],
+                                                         label_smoothing=cfg.label_smoothing, loss_weights=lw)
+    labels = ref_obj.termination_distance_bucket_labels(y, stop_ids=A["stop_ids"], bucket_edges=A["bucket_edges"])
+    cw = torch.tensor(A["term_class_weights"])
+    term_loss = ref_obj.termination_aux_loss(aux["termination_logits"], labels, class_weights=cw)
+    total = loss + off_total + A["term_weight"] * term_loss
+    total.backward()
+    out = {"config": np.array(json.dumps(cfg.to_dict())), "objective": np.array(json.dumps(
+        {k: (list(v) if isinstance(v, tuple) else ({str(a): b for a, b in v.items()} if isinstance(v, dict) else v))
+         for k, v in A.items()})), "idx": idx, "targets": tgt,
+        "loss": np.array(loss.item()), "total": np.array(total.item()), "term_loss": np.array(term_loss.item()),
+        "term_labels": labels.numpy(), "termination_logits": aux["termination_logits"].detach().numpy()}
+    for k, v in off_losses.items():
+        out[f"offset_loss_{k}"] = np.array(v.item())
+    for k, v in aux["offset_logits"].items():
+        out[f"offset_logits_{k}"] = v.detach().numpy()
+    for k, v in params.items():
+        out[f"param/{k}"] = v
+    for k, p in model.named_parameters():
+        out[f"grad/{k}"] = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().numpy().copy()
+    np.savez_compressed(HERE / "aux_objective.npz", **out)
+    print(f"[golden] aux_objective: total={total.item():.6f}")
+
+
 def main():
     torch.set_num_threads(8)
+    only = set(sys.argv[1:])
+    if only:  # regenerate selected fixtures only, e.g. `make_golden.py aux_objective`
+        if "aux_objective" in only:
+            aux_objective_case()
+        if "objectives" in only:
+            objectives_case()
+        return
     c1 = OracleConfig(vocab_size=68, block_size=64, n_layer=2, n_head=4, n_embd=64,
                       label_smoothing=0.05, sep_id=3)
     run_case("mha_gelu_sep", c1, 2, 64, sep_every=20, pad_tail=9, adamw=True)
@@ -233,6 +285,7 @@ def main():
                       label_smoothing=0.05)
     run_case("c4_layer", c7, 1, 1024, sep_every=330, store_params=False, store_grads=False)
     objectives_case()
+    aux_objective_case()
 
 
 if __name__ == "__main__":

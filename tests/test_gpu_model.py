@@ -27,6 +27,8 @@ def make_model(cfgd, g, dtype="fp32", dropout=0.0):
     m = TinyGPT(cfg.vocab_size, cfg.block_size, n_layer=cfg.n_layer, n_head=cfg.n_head, n_embd=cfg.n_embd,
                 dropout=dropout, label_smoothing=cfg.label_smoothing, sep_id=cfg.sep_id,
                 tie_embeddings=cfg.tie_embeddings, n_kv_head=cfg.n_kv_head, loss_weights=cfg.loss_weights,
+                termination_aux=cfg.termination_aux, termination_n_classes=cfg.termination_n_classes,
+                multi_offset_targets=cfg.multi_offset_targets or None,
                 use_swiglu=cfg.use_swiglu, use_rope=cfg.use_rope, compute_dtype=dtype, device=DEV)
     sd = {k: torch.from_numpy(v) for k, v in params.items()}
     missing, unexpected = m.load_state_dict(sd, strict=False)

@@ -131,6 +131,32 @@ def test_oracle_objectives_and_schedule():
     assert abs(total - float(g["mo_total"])) < 1e-5
 
 
+def aux_objective_args(g):
+    import json
+    obj = json.loads(str(g["objective"]))
+    return dict(offset_weights={int(k): float(v) for k, v in obj["offset_weights"].items()},
+                term_weight=float(obj["term_weight"]), stop_ids=tuple(obj["stop_ids"]),
+                bucket_edges=tuple(obj["bucket_edges"]), term_class_weights=obj["term_class_weights"])
+
+
+def test_oracle_aux_objective_matches_reference():
+    """next-codon CE + multi-offset + termination objective and all its grads (loop.py:1075-1112)."""
+    cfgd, g = load_golden("aux_objective")
+    cfg = _cfg(cfgd)
+    params = _params(cfg, g, 0)
+    parts, grads = O.objective_backward(cfg, params, g["idx"], g["targets"], **aux_objective_args(g))
+    assert np.array_equal(parts["term_labels"], g["term_labels"])
+    for key in ("loss", "total", "term_loss", "offset_loss_2", "offset_loss_4"):
+        assert abs(float(parts[key]) - float(g[key])) <= 2e-6 * max(1.0, abs(float(g[key]))), key
+    for k, v in grads.items():
+        ref = g[f"grad/{k}"]
+        s = max(1e-3, float(np.abs(ref).max()))
+        assert np.abs(v.numpy() - ref).max() <= 1e-4 * s, k
+    # the aux heads do receive gradient in this objective
+    assert np.abs(g["grad/termination_head.weight"]).max() > 0
+    assert np.abs(g["grad/offset_projs.2.0.weight"]).max() > 0
+
+
 def test_dropout_hash_statistics():
     keep = O.dropout_keep(1234, np.arange(256)[:, None], np.arange(1024)[None, :], 0.1)
     frac = 1.0 - keep.mean()
