@@ -109,7 +109,9 @@ SIGNATURES = {
     "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),
     "cg_cast_pad_2d": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp]),
-    "cg_offset_targets": (i32, [vp, i32, i32, i32, C.POINTER(i32), i32, vp, vp, vp]),
+    "cg_gather_windows": (i32, [i32, vp, i64, i64, vp, i32, i32, vp, vp]),
+    "cg_gather_sequences": (i32, [i32, vp, vp, vp, i64, vp, i32, i32, vp, vp, vp]),
+    "cg_offset_targets":(i32, [vp, i32, i32, i32, C.POINTER(i32), i32, vp, vp, vp]),
     "cg_termination_labels": (i32, [vp, i32, i32, C.POINTER(i32), i32, C.POINTER(i32), i32, i32, vp, vp]),
     "cg_adamw": (i32, [vp, vp, vp, vp, vp, C.POINTER(AdamwSegment), i32, f32, f32, f32, i32, f32, vp]),
     "cg_nonfinite_flag": (i32, [vp, i64, vp, vp]),

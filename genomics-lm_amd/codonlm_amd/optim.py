@@ -59,6 +59,21 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         self.model.zero_grad(set_to_none)
 
+    def state_dict(self):
+        """torch's param_groups (lr/wd the schedulers drive) + the flat moments and step."""
+        sd = super().state_dict()
+        sd["flat_state"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": int(self.step_count)}
+        return sd
+
+    def load_state_dict(self, state_dict):
+        flat = state_dict.get("flat_state")
+        super().load_state_dict({k: v for k, v in state_dict.items() if k != "flat_state"})
+        if flat is not None:
+            with torch.no_grad():
+                self.exp_avg.copy_(flat["exp_avg"])
+                self.exp_avg_sq.copy_(flat["exp_avg_sq"])
+            self.step_count = int(flat["step"])
+
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):
         loss = closure() if closure is not None else None

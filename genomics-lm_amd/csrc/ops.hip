@@ -1055,6 +1055,79 @@ extern "C" int cg_cast_pad_2d(const float* src, long long lds, int rows, int col
 }
 
 // ===========================================================================
+// Device-resident codon batches (src/codonlm/data_loading.py PackedDataset :43-129 and
+// dynamic_lm_collate_fn :380-393): token rows gathered from HBM by sample index, widened to
+// int64 and (dynamic layout) shifted into x = seq[:-1], y = seq[1:] with a PAD tail.
+// Out-of-range sample indices produce PAD rows instead of faulting.
+// ===========================================================================
+template <typename T_>
+__global__ __launch_bounds__(256) void gather_windows_kernel(const T_* __restrict__ X, long long ldx, long long nrows,
+                                                             const int64_t* __restrict__ rows, int B, int T,
+                                                             int64_t* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * T) return;
+  const int b = (int)(i / T), t = (int)(i - (long long)b * T);
+  const int64_t r = rows[b];
+  out[i] = (r >= 0 && r < nrows) ? (int64_t)X[r * ldx + t] : 0;
+}
+extern "C" int cg_gather_windows(int elem_bytes, const void* X, long long ldx, long long nrows, const int64_t* rows,
+                                 int B, int T, int64_t* out, void* stream) {
+  if (B < 0 || T < 0 || ldx < T || nrows < 0) return CG_EINVAL;
+  const long long total = (long long)B * T;
+  if (total == 0) return CG_OK;
+  if (!X || !rows || !out) return CG_EINVAL;
+  const dim3 g((unsigned)((total + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  switch (elem_bytes) {
+    case 1: hipLaunchKernelGGL(gather_windows_kernel<uint8_t>, g, dim3(256), 0, s, (const uint8_t*)X, ldx, nrows, rows, B, T, out); break;
+    case 2: hipLaunchKernelGGL(gather_windows_kernel<int16_t>, g, dim3(256), 0, s, (const int16_t*)X, ldx, nrows, rows, B, T, out); break;
+    case 4: hipLaunchKernelGGL(gather_windows_kernel<int32_t>, g, dim3(256), 0, s, (const int32_t*)X, ldx, nrows, rows, B, T, out); break;
+    case 8: hipLaunchKernelGGL(gather_windows_kernel<int64_t>, g, dim3(256), 0, s, (const int64_t*)X, ldx, nrows, rows, B, T, out); break;
+    default: return CG_EUNSUPPORTED;
+  }
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+template <typename T_>
+__global__ __launch_bounds__(256) void gather_sequences_kernel(const T_* __restrict__ flat,
+                                                               const int64_t* __restrict__ starts,
+                                                               const int64_t* __restrict__ lens, long long nseq,
+                                                               const int64_t* __restrict__ rows, int B, int Tout,
+                                                               int64_t* __restrict__ x, int64_t* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)B * Tout) return;
+  const int b = (int)(i / Tout), t = (int)(i - (long long)b * Tout);
+  const int64_t r = rows[b];
+  int64_t xv = 0, yv = 0;
+  if (r >= 0 && r < nseq && t + 1 < lens[r]) {
+    const T_* s = flat + starts[r];
+    xv = (int64_t)s[t];
+    yv = (int64_t)s[t + 1];
+  }
+  x[i] = xv;
+  y[i] = yv;
+}
+extern "C" int cg_gather_sequences(int elem_bytes, const void* flat, const int64_t* starts, const int64_t* lens,
+                                   long long nseq, const int64_t* rows, int B, int Tout, int64_t* x, int64_t* y,
+                                   void* stream) {
+  if (B < 0 || Tout < 0 || nseq < 0) return CG_EINVAL;
+  const long long total = (long long)B * Tout;
+  if (total == 0) return CG_OK;
+  if (!flat || !starts || !lens || !rows || !x || !y) return CG_EINVAL;
+  const dim3 g((unsigned)((total + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  switch (elem_bytes) {
+    case 1: hipLaunchKernelGGL(gather_sequences_kernel<uint8_t>, g, dim3(256), 0, s, (const uint8_t*)flat, starts, lens, nseq, rows, B, Tout, x, y); break;
+    case 2: hipLaunchKernelGGL(gather_sequences_kernel<int16_t>, g, dim3(256), 0, s, (const int16_t*)flat, starts, lens, nseq, rows, B, Tout, x, y); break;
+    case 4: hipLaunchKernelGGL(gather_sequences_kernel<int32_t>, g, dim3(256), 0, s, (const int32_t*)flat, starts, lens, nseq, rows, B, Tout, x, y); break;
+    case 8: hipLaunchKernelGGL(gather_sequences_kernel<int64_t>, g, dim3(256), 0, s, (const int64_t*)flat, starts, lens, nseq, rows, B, Tout, x, y); break;
+    default: return CG_EUNSUPPORTED;
+  }
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
 // Auxiliary objectives' labels (src/codonlm/training/objectives.py): integer work, one
 // thread per (b, t), ids passed by value.
 // ===========================================================================

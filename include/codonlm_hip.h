@@ -170,6 +170,19 @@ int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stre
 int cg_cast_pad_2d(const float* src, long long lds, int rows, int cols, int dtype, void* dst,
                    long long ldd, int dcols, void* stream);
 
+/* Device-resident batches (src/codonlm/data_loading.py): the token arrays live in HBM and a
+ * batch is one gather launch (no per-step host->device copy of tokens).  elem_bytes: 1
+ * (uint8), 2 (int16), 4 (int32) or 8 (int64) storage, widened to int64.
+ * fixed windows (PackedDataset X/Y :43-129): out[b][t] = X[rows[b]][t]
+ * dynamic sequences (flat X + lengths, dynamic_lm_collate_fn :380-393): x[b][t] = seq[t],
+ * y[b][t] = seq[t+1] for t < len-1, PAD (0) beyond; seq = flat[starts[r] .. +lens[r]).
+ * rows: device int64 sample indices; out-of-range rows give PAD rows. */
+int cg_gather_windows(int elem_bytes, const void* X, long long ldx, long long nrows,
+                      const int64_t* rows, int B, int T, int64_t* out, void* stream);
+int cg_gather_sequences(int elem_bytes, const void* flat, const int64_t* starts,
+                        const int64_t* lens, long long nseq, const int64_t* rows, int B, int Tout,
+                        int64_t* x, int64_t* y, void* stream);
+
 /* Auxiliary objectives' label construction (src/codonlm/training/objectives.py).
  * offset targets (offset_target_mask :6-23): out[b][t] = y[b][t+k-1] where that target is
  * valid (t+k-1 < T, not PAD, no boundary id among y[b][t..t+k-2]), else 0 (= ignored by the

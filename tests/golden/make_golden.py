@@ -253,12 +253,58 @@ def aux_objective_case():
     print(f"[golden] aux_objective: total={total.item():.6f}")
 
 
+def data_order_case():
+    """Batch order of the reference loaders (data_loading.py:332-486): a fixed-window NPZ
+    through build_codon_lm_dataloaders (seeded RandomSampler) and a dynamic NPZ through the
+    BucketBatchSampler + dynamic collate; stored as the batches the reference yields."""
+    import tempfile
+    from src.codonlm.data_loading import PackedDataset, build_codon_lm_dataloaders  # noqa: E402 (reference)
+    out = {}
+    with tempfile.TemporaryDirectory() as td:
+        n, T = 23, 5
+        X = np.arange(n * T, dtype=np.int32).reshape(n, T) % 60 + 4
+        X[:, 0] = np.arange(n) + 4
+        Y = (X + 1).astype(np.int32)
+        fx = os.path.join(td, "fixed.npz")
+        np.savez_compressed(fx, X=X, Y=Y)
+        ds = PackedDataset([fx])
+        for seed in (11, 12):
+            tl, vl, _, _ = build_codon_lm_dataloaders(ds, ds, {"batch_size": 4, "dataloader_seed": seed})
+            out[f"fixed_seed{seed}_x"] = np.concatenate([xb.numpy() for xb, _ in tl])
+            out[f"fixed_seed{seed}_sizes"] = np.array([xb.shape[0] for xb, _ in tl])
+        out["fixed_val_x"] = np.concatenate([xb.numpy() for xb, _ in vl])
+        rng = np.random.default_rng(5)
+        lens = rng.integers(3, 20, size=37)
+        flat = rng.integers(4, 68, size=int(lens.sum())).astype(np.int32)
+        fd = os.path.join(td, "dyn.npz")
+        np.savez_compressed(fd, X=flat, lengths=lens)
+        dds = PackedDataset([fd])
+        tl, vl, sampler, _ = build_codon_lm_dataloaders(dds, dds, {"batch_size": 3, "dataloader_seed": 9,
+                                                                    "bucket_batching": True, "n_buckets": 4})
+        xs, ys = [], []
+        for xb, yb in tl:
+            xs.append(xb.numpy())
+            ys.append(yb.numpy())
+        out["dyn_flat"], out["dyn_lengths"] = flat, lens
+        out["dyn_bucket_batches"] = np.array(len(xs))
+        for i, (xa, ya) in enumerate(zip(xs, ys)):
+            out[f"dyn_bucket_x_{i}"], out[f"dyn_bucket_y_{i}"] = xa, ya
+        vx = [xb.numpy() for xb, _ in vl]
+        out["dyn_val_batches"] = np.array(len(vx))
+        for i, xa in enumerate(vx):
+            out[f"dyn_val_x_{i}"] = xa
+    np.savez_compressed(HERE / "data_order.npz", **out)
+    print("[golden] data_order")
+
+
 def main():
     torch.set_num_threads(8)
     only = set(sys.argv[1:])
     if only:  # regenerate selected fixtures only, e.g. `make_golden.py aux_objective`
         if "aux_objective" in only:
             aux_objective_case()
+        if "data_order" in only:
+            data_order_case()
         if "objectives" in only:
             objectives_case()
         return
@@ -286,6 +332,7 @@ def main():
     run_case("c4_layer", c7, 1, 1024, sep_every=330, store_params=False, store_grads=False)
     objectives_case()
     aux_objective_case()
+    data_order_case()
 
 
 if __name__ == "__main__":
