@@ -111,6 +111,7 @@ SIGNATURES = {
     "cg_cast_pad_2d": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp]),
     "cg_gather_windows": (i32, [i32, vp, i64, i64, vp, i32, i32, vp, vp]),
     "cg_gather_sequences": (i32, [i32, vp, vp, vp, i64, vp, i32, i32, vp, vp, vp]),
+    "cg_pool_hidden": (i32, [i32, vp, i64, vp, i32, i32, i32, i32, i32, C.POINTER(u32), vp, vp]),
     "cg_offset_targets":(i32, [vp, i32, i32, i32, C.POINTER(i32), i32, vp, vp, vp]),
     "cg_termination_labels": (i32, [vp, i32, i32, C.POINTER(i32), i32, C.POINTER(i32), i32, i32, vp, vp]),
     "cg_adamw": (i32, [vp, vp, vp, vp, vp, C.POINTER(AdamwSegment), i32, f32, f32, f32, i32, f32, vp]),

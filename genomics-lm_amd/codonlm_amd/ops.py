@@ -211,6 +211,30 @@ def termination_labels(y, stop_ids, bucket_edges=(0, 3, 10, 30), ignore_index=-1
     return out
 
 
+POOL_MODES = {"mean_nonpad": 0, "mean_content": 1, "eos": 2}
+
+
+def pool_hidden(hidden, idx, mode, content_ids=(), pad_id=0):
+    """_pool_state (extract_embeddings.py:94-114) of hidden (B, T, d) -> fp32 (B, d)."""
+    L.require_device(hidden, "pool_hidden")
+    B, T, d = hidden.shape
+    if hidden.stride(2) != 1 or hidden.stride(0) != T * hidden.stride(1):
+        hidden = hidden.contiguous()
+    idx = idx.to(device=hidden.device, dtype=torch.int64).contiguous()
+    words = [0] * 8
+    for t in content_ids:
+        t = int(t)
+        if not 0 <= t < 256:
+            raise ValueError("content ids must be in [0, 256)")
+        words[t >> 5] |= 1 << (t & 31)
+    mask = (C.c_uint32 * 8)(*words)
+    out = torch.empty(B, d, dtype=torch.float32, device=hidden.device)
+    L.check(L.lib.cg_pool_hidden(_dt(hidden), hidden.data_ptr(), hidden.stride(1), idx.data_ptr(), B, T, d,
+                                 int(pad_id), POOL_MODES[mode], mask, out.data_ptr(),
+                                 L.stream_ptr(hidden.device)), "cg_pool_hidden")
+    return out
+
+
 def colsum(x, out=None, accumulate=False):
     """out[n] (+)= sum_m x[m, n] (fp32 out)."""
     L.require_device(x, "colsum")

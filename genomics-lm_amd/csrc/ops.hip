@@ -1128,6 +1128,66 @@ extern "C" int cg_gather_sequences(int elem_bytes, const void* flat, const int64
 }
 
 // ===========================================================================
+// Sequence pooling of hidden states (scripts/extract_embeddings.py _pool_state :94-114):
+// mode 0 mean over non-PAD positions, 1 mean over content-token positions (id bitmask),
+// 2 state at position (#non-PAD - 1).  One thread per (sequence, feature); the token ids of a
+// row are read once per wave from L1/L2, the states coalesced along the feature axis.
+// ===========================================================================
+struct TokMask {
+  uint32_t w[8];  // ids 0..255
+};
+template <typename T_>
+__global__ __launch_bounds__(256) void pool_hidden_kernel(const T_* __restrict__ h, long long ldh,
+                                                          const int64_t* __restrict__ idx, int T, int d, int pad,
+                                                          int mode, TokMask cm, float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= d) return;
+  const int64_t* row = idx + (long long)b * T;
+  const T_* hb = h + (long long)b * T * ldh + c;
+  if (mode == 2) {
+    int n = 0;
+    for (int t = 0; t < T; ++t) n += row[t] != pad;
+    const int pos = n > 0 ? n - 1 : 0;
+    out[(long long)b * d + c] = ld_act<T_>(hb + (long long)pos * ldh);
+    return;
+  }
+  float s = 0.f, cnt = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const int64_t v = row[t];
+    bool w;
+    if (mode == 0)
+      w = v != pad;
+    else
+      w = v >= 0 && v < 256 && ((cm.w[v >> 5] >> (v & 31)) & 1u);
+    if (w) {
+      s += ld_act<T_>(hb + (long long)t * ldh);
+      cnt += 1.f;
+    }
+  }
+  out[(long long)b * d + c] = s / fmaxf(cnt, 1.f);
+}
+extern "C" int cg_pool_hidden(int dtype, const void* h, long long ldh, const int64_t* idx, int B, int T, int d,
+                              int pad_id, int mode, const uint32_t* content_mask, float* out, void* stream) {
+  if (B < 0 || T < 0 || d < 0 || ldh < d || mode < 0 || mode > 2) return CG_EINVAL;
+  if ((long long)B * d == 0) return CG_OK;
+  if (!h || !idx || !out || (mode == 1 && !content_mask)) return CG_EINVAL;
+  TokMask cm;
+  for (int i = 0; i < 8; ++i) cm.w[i] = content_mask ? content_mask[i] : 0u;
+  const dim3 g(cg_cdiv(d, 256), B);
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(pool_hidden_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)h, ldh, idx, T,
+                       d, pad_id, mode, cm, out);
+  else if (dtype == CG_F32)
+    hipLaunchKernelGGL(pool_hidden_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)h, ldh, idx, T, d,
+                       pad_id, mode, cm, out);
+  else
+    return CG_EUNSUPPORTED;
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ===========================================================================
 // Auxiliary objectives' labels (src/codonlm/training/objectives.py): integer work, one
 // thread per (b, t), ids passed by value.
 // ===========================================================================

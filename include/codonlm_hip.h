@@ -183,6 +183,15 @@ int cg_gather_sequences(int elem_bytes, const void* flat, const int64_t* starts,
                         const int64_t* lens, long long nseq, const int64_t* rows, int B, int Tout,
                         int64_t* x, int64_t* y, void* stream);
 
+/* Sequence embeddings from hidden states (scripts/extract_embeddings.py _pool_state :94-114):
+ * h: [B*T rows][ldh] (dtype) as cg_model_hidden returns; out fp32 [B][d].
+ * mode 0 = mean over idx != pad_id, 1 = mean over ids set in content_mask (host, 8 x 32-bit
+ * words = ids 0..255), 2 = the state at position (#non-PAD - 1, clamped at 0). */
+enum { CG_POOL_MEAN_NONPAD = 0, CG_POOL_MEAN_CONTENT = 1, CG_POOL_EOS = 2 };
+int cg_pool_hidden(int dtype, const void* h, long long ldh, const int64_t* idx, int B, int T,
+                   int d, int pad_id, int mode, const uint32_t* content_mask, float* out,
+                   void* stream);
+
 /* Auxiliary objectives' label construction (src/codonlm/training/objectives.py).
  * offset targets (offset_target_mask :6-23): out[b][t] = y[b][t+k-1] where that target is
  * valid (t+k-1 < T, not PAD, no boundary id among y[b][t..t+k-2]), else 0 (= ignored by the

@@ -1,0 +1,159 @@
+"""Inference CLIs on the MI355X: extract_embeddings and query_model.
+
+Parity: the pooling kernel is checked directly against the reference's own pooled
+embeddings (golden ``pooled/{layer}/{mode}`` of mha_gelu_sep / hd48_gqa, produced by the
+reference's _pool_state algorithm on its iter_hidden_states); the CLIs are checked end to
+end against the oracle (itself pinned by those fixtures) on a run directory written here.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import tinygpt_oracle as O
+from test_gpu_model import DEV, make_model, _idx
+
+pytestmark = pytest.mark.gpu
+
+FASTA = """>g1 short
+ATGAAACCCGGGTTTTAA
+>g2 lower-case rna
+augcccuuuaaagggcccuuuaaagggcccugu
+>g3 with unknown codon
+ATGNNNAAACCCTAG
+>g4 long (truncated at block_size)
+{long}
+>g5
+ATGGCTGCAGCCGCGTGA
+>g6 odd length
+ATGAAACCCGG
+>g7
+ATGTTTTTCTTATTGTCTTCCTCATCGTAA
+"""
+VOCAB = ["<PAD>", "<BOS_CDS>", "<EOS_CDS>", "<SEP>"] + [a + b + c for a in "ACGT" for b in "ACGT" for c in "ACGT"]
+
+
+@pytest.mark.parametrize("case", ["mha_gelu_sep", "hd48_gqa"])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_pool_kernel_matches_reference_pooling(case, dtype):
+    from codonlm_amd import ops
+    cfgd, g = load_golden(case)
+    m, cfg, _ = make_model(cfgd, g, dtype=dtype)
+    m.eval()
+    x, _ = _idx(g)
+    eng = m.engine
+    eng.forward(x, None, training=False)
+    for layer in list(range(cfg.n_layer + 1)) + ["final"]:
+        h = eng.hidden(cfg.n_layer + 1 if layer == "final" else layer)
+        for mode in ("mean_nonpad", "mean_content", "eos"):
+            got = ops.pool_hidden(h, x, mode, range(4, 68)).cpu().numpy()
+            ref = g[f"pooled/{layer}/{mode}"]
+            s = max(1.0, float(np.abs(g[f"hidden/{layer}"]).max()))
+            if dtype == "fp32":
+                assert float(np.abs(got - ref).max()) <= 2e-5 * s, (layer, mode)
+            else:  # same pooling of the bf16/fp32 engine states, exact up to fp32 summation order
+                exp = O.pool_state(h.float().cpu(), g["idx"], mode, list(range(4, 68))).numpy()
+                assert float(np.abs(got - exp).max()) <= 1e-5 * s, (layer, mode)
+
+
+def _write_run(tmp_path):
+    cfg = O.OracleConfig(vocab_size=68, block_size=64, n_layer=2, n_head=2, n_embd=128, sep_id=3)
+    params = O.synthetic_params(cfg, seed=2024)
+    run_cfg = {"vocab_size": 68, "block_size": 64, "n_layer": 2, "n_head": 2, "n_embd": 128, "dropout": 0.1,
+               "sep_mask_enabled": True, "tie_embeddings": True}
+    rd = tmp_path / "run"
+    (rd / "checkpoints").mkdir(parents=True)
+    (rd / "itos.txt").write_text("\n".join(VOCAB) + "\n")
+    sd = {k: torch.from_numpy(v) for k, v in params.items()}
+    sd["head.weight"] = sd["tok_emb.weight"]
+    torch.save({"model": sd, "cfg": run_cfg}, rd / "checkpoints" / "best.pt")
+    rng = np.random.default_rng(8)
+    long_seq = "ATG" + "".join(rng.choice(["AAA", "CCC", "GGT", "TTG", "GCA"], size=90)) + "TAA"
+    fa = tmp_path / "in.fasta"
+    fa.write_text(FASTA.format(long=long_seq))
+    return rd, fa, cfg, params
+
+
+def test_extract_embeddings_cli_matches_oracle(tmp_path):
+    from codonlm_amd import extract_embeddings as ex
+    rd, fa, cfg, params = _write_run(tmp_path)
+    outs = {}
+    for bs in (3, 1):
+        out = tmp_path / f"emb_bs{bs}.npz"
+        ex.main(["--run_dir", str(rd), "--fasta", str(fa), "--batch-size", str(bs), "--hidden-layers",
+                 "0,1,2,final", "--pooling-modes", "mean_nonpad,mean_content,eos", "--out", str(out)])
+        with np.load(out, allow_pickle=True) as z:  # written by this test (ids is an object array)
+            outs[bs] = {k: z[k] for k in z.files}
+    meta = json.loads((tmp_path / "emb_bs3.npz.metadata.json").read_text())
+    assert sorted(meta) == sorted([
+        "schema_version", "validation_status", "created_at", "checkpoint", "model_weights", "dataset_manifest",
+        "checkpoint_dataset", "vocabulary", "inputs", "mask_mode", "pooling_mode", "representations",
+        "shape_guidance", "block_size", "extraction_batch_size", "truncation_policy", "code_git_sha"])
+    assert meta["mask_mode"] == "canonical_causal_segment" and meta["pooling_mode"] == "multi_representation"
+    z = outs[3]
+    assert list(z["ids"]) == ["g1 short", "g2 lower-case rna", "g3 with unknown codon",
+                              "g4 long (truncated at block_size)", "g5", "g6 odd length", "g7"]
+    stoi = {t: i for i, t in enumerate(VOCAB)}
+    seqs = ex.read_fasta(fa)
+    examples = ex.tokenize(seqs, stoi, "dna_cds", 64)
+    assert examples[2][1] == [1, stoi["ATG"], stoi["AAA"], stoi["CCC"], stoi["TAG"], 2]  # NNN dropped
+    assert len(examples[3][1]) == 64  # right-truncated at block_size
+    content = [i for i, t in enumerate(VOCAB) if len(t) == 3 and t.isalpha()]
+    for i, (_, toks) in enumerate(examples):
+        idx = np.array([toks])
+        states = dict(O.iter_hidden_states(cfg, params, idx))
+        for layer in (0, 1, 2, "final"):
+            for mode in ("mean_nonpad", "mean_content", "eos"):
+                ref = O.pool_state(states[layer], idx, mode, content).numpy()[0]
+                got = z[f"X__layer_{layer}__{mode}"][i]
+                s = max(1.0, float(np.abs(states[layer].numpy()).max()))
+                assert float(np.abs(got - ref).max()) <= 5e-5 * s, (i, layer, mode)
+                # padding-independent: batch 1 and batch 3 agree
+                assert float(np.abs(got - outs[1][f"X__layer_{layer}__{mode}"][i]).max()) <= 2e-5 * s
+
+
+def test_query_model_next_score_and_greedy_match_oracle(tmp_path):
+    from types import SimpleNamespace
+    from codonlm_amd import query_model as Q
+    rd, _, cfg, params = _write_run(tmp_path)
+    itos, stoi = Q._load_vocab(rd)
+    sd, run_cfg = Q._load_checkpoint(rd)
+    model = Q.build_model_from_state(sd, run_cfg)
+    device = Q.dev()
+    for dna in ("ATGAAACCCGGG", "atgcccuuuaaagggccc", "ATGGCTGCAGCCGCGTGAAAA"):
+        ids = Q.dna_to_ids(dna, stoi)
+        assert ids[-1] == stoi["<EOS_CDS>"]  # the reference appends EOS even in next mode
+        ans = Q._answer(dna, SimpleNamespace(mode="next", topk=5), itos, stoi, model, device)
+        with torch.no_grad():
+            o = O.forward(cfg, params, np.array([ids]))
+        p = torch.softmax(o["logits"][0, -1], -1)
+        topv, topi = torch.topk(p, 5)
+        assert [t["token"] for t in ans["topk"]] == [itos[i] for i in topi.tolist()]
+        np.testing.assert_allclose([t["prob"] for t in ans["topk"]], topv.numpy(), rtol=1e-4, atol=1e-6)
+        sc = Q._answer(dna, SimpleNamespace(mode="score", topk=5), itos, stoi, model, device)
+        with torch.no_grad():
+            ref = O.forward(cfg, params, np.array([ids[:-1]]), np.array([ids[1:]]))["loss"].item()
+        assert abs(sc["nll"] - ref) <= 1e-4 * max(1.0, abs(ref))
+    assert Q._answer("AT", SimpleNamespace(mode="next", topk=5), itos, stoi, model, device) == \
+        {"error": "prompt too short (<3 nt)"}
+    with pytest.raises(ValueError, match="Unknown codon"):
+        Q.dna_to_ids("ATGNNN", stoi)
+    # greedy continuation: ids bit-exact vs the oracle's argmax at every step (70 > block_size
+    # exercises the context truncation)
+    ctx = Q.dna_prefix_to_ids("ATGAAACCC", stoi)
+    got = Q.greedy_generate(model, device, ctx, max_new=70)
+    full = list(ctx)
+    for _ in range(70):
+        with torch.no_grad():
+            logits = O.forward(cfg, params, np.array([full[-64:]]))["logits"][0, -1]
+        nxt_ref = int(torch.argmax(logits))
+        nxt = int(torch.argmax(Q.next_token(model, device, full)).item())
+        if nxt != nxt_ref:  # only an unresolvable top-2 tie may differ
+            top2 = torch.topk(logits, 2).values
+            assert float(top2[0] - top2[1]) < 1e-3, (len(full), nxt, nxt_ref)
+            break
+        full.append(nxt)
+    else:
+        assert got == full[-64:]
