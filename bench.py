@@ -216,6 +216,15 @@ def main():
                               "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                               "traffic": None, "launches": k, "avg_launch_us": round(ms / k * 1e3, 2),
                               "measured": "HIP events on the launch stream around every launch in the timed region"}
+        # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
+        # (profiles/<round>/pmc_traffic.json; FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections)
+        tr = ROOT / "profiles" / "round1" / "pmc_traffic.json"
+        if tr.exists() and args.config == "c4" and (B == CONFIGS["c4"]["batch"]):
+            t = json.loads(tr.read_text())
+            if t.get("probe") == L.PROBE_NAMES[dominant]:
+                result["roofline"]["traffic"] = t["hbm_bytes_per_launch"]
+                result["roofline"]["traffic_unit"] = "HBM bytes/launch (PMC)"
+                result["roofline"]["traffic_source"] = "profiles/round1/pmc_traffic.json"
         result["kernels"] = {
             L.PROBE_NAMES[kk]: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None,
                                 "ms_per_step": round(v[1] / 2, 3), "launches_per_step": v[2] // 2}
