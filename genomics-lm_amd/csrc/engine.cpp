@@ -153,7 +153,7 @@ struct Acts {
   std::vector<void*> oa, og, opj;
 };
 
-constexpr int MAX_SPLIT = 8;
+constexpr int MAX_SPLIT = 16;
 
 size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Acts& A) {
   WS w{base, 0};
@@ -341,7 +341,9 @@ int pick_split(const Ctx& C, int Mo, int N, long long K) {
   long long s = (512 + tiles - 1) / tiles;
   long long smax = K / 512;
   if (s > smax) s = smax;
-  if (s > MAX_SPLIT) s = MAX_SPLIT;
+  // 8 slabs suffice once there are >= 32 tiles; the 16-tile products (d x d at d512: attention
+  // proj) run 218 -> 291 TF/s with 16 (dw_sweep on the box)
+  if (s > (tiles > 16 ? 8 : MAX_SPLIT)) s = tiles > 16 ? 8 : MAX_SPLIT;
   if (s < 1) s = 1;
   if ((size_t)s * Mo * N > C.A.splitws_floats) s = 1;
   return (int)s;
