@@ -657,8 +657,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(cg_gemm(&g, C.s));
       CK(cg_colsum_reduce(A.splitws, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
       CK(lin_dw(C, A.dbig, D.hid, a.h2, d, D.hid, d, o.w1, d, accumulate));
-      g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dtmp, d, a.w1T);
-      g.c_dtype = CG_F32;
+      g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
       CK(cg_gemm(&g, C.s));
     } else {
       CK(lin_dw(C, A.gT, d, a.s, D.Hp, d, D.Hp, o.wd, D.Hp, accumulate));
@@ -666,12 +665,11 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(cg_gemm(&g, C.s));
       CK(cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, A.dbig, 2 * D.Hp, (int)M, D.hid, C.s));
       CK(lin_dw(C, A.dbig, 2 * D.Hp, a.h2, d, 2 * D.Hp, d, o.wgu, d, accumulate));
-      g = lin_dx(C, A.dbig, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dtmp, d, a.wguT);
-      g.c_dtype = CG_F32;
+      g = lin_dx(C, A.dbig, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dsmall, d, a.wguT);
       CK(cg_gemm(&g, C.s));
     }
     // gT = dL/d(proj out); its column sum is the proj bias gradient
-    CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, A.gT, 0, 0.f,
+    CK(cg_layernorm_bwd(C.dt, A.dsmall, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, A.gT, 0, 0.f,
                         A.lnpart, G(C, o.ln2w), G(C, o.ln2b), G(C, o.bp), accumulate, (int)M, d, eps, C.s));
     // ---------------- attention branch
     CK(lin_dw(C, A.gT, d, a.y, d, d, d, o.wp, d, accumulate));
@@ -683,13 +681,12 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(cg_rope_tab(C.dt, A.dbig, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
     CK(lin_dw(C, A.dbig, D.Nqkv, a.h1, d, D.Nqkv, d, o.wqkv, d, accumulate));
     CK(bias_grad(C, A.dbig, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
-    g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dtmp, d, a.qkvT);
-    g.c_dtype = CG_F32;
+    g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
     CK(cg_gemm(&g, C.s));
     // gT feeds block l-1's MLP output Linear (bias grad fused as above; lands in block l-1's
     // gradient range, which is all-reduced only after phase l-1)
     float* db2 = (l > 0 && !D.swiglu) ? G(C, C.Lo.lay[l - 1].b2) : nullptr;
-    CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xl, d, a.mean1, a.rstd1, P(C, o.ln1w), A.g, A.g, C.dt,
+    CK(cg_layernorm_bwd(C.dt, A.dsmall, d, xl, d, a.mean1, a.rstd1, P(C, o.ln1w), A.g, A.g, C.dt,
                         l > 0 ? A.gT : nullptr, site_seed(seed, l - 1, SITE_MLP), l > 0 ? p : 0.f, A.lnpart,
                         G(C, o.ln1w), G(C, o.ln1b), db2, accumulate, (int)M, d, eps, C.s));
     return CG_OK;
