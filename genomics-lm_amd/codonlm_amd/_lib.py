@@ -121,6 +121,12 @@ SIGNATURES = {
     "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
     "cg_model_aux_forward": (i32, [C.POINTER(Model), vp, i64, C.POINTER(vp), vp]),
     "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),
+    "cg_kv_cache_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
+    "cg_decode_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32]),
+    "cg_model_prefill": (i32, [C.POINTER(Model), vp, i32, i32, i32, vp, i32, vp, vp, vp]),
+    "cg_model_decode": (i32, [C.POINTER(Model), vp, i32, i32, vp, i32, vp, vp, sz, vp, vp]),
+    "cg_attn_decode": (i32, [i32, vp, i64, vp, i64, i32, i32, vp, i32, i32, i32, i32, i32, vp, i64, vp]),
+    "cg_segstate_step": (i32, [vp, i32, i32, i32, vp, vp]),
     "cg_model_hidden": (vp, [C.POINTER(Model), i32, C.POINTER(i32), C.POINTER(i64)]),
     "cg_probe_enable": (i32, [i32]),
     "cg_probe_read": (i32, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)]),

@@ -223,6 +223,10 @@ class Engine:
             m.d_offset_logits[i] = t.data_ptr()
         self._grad_keep = keep  # alive until the backward kernels are enqueued
 
+    # -- incremental decoding (KV cache) -------------------------------------------------
+    def new_kv_cache(self, B: int, Tmax: int | None = None) -> "KVCache":
+        return KVCache(self, B, Tmax or self.cfg.block_size)
+
     def backward_phase(self, phase: int, layer: int = 0, accumulate: bool = False):
         st = L.stream_ptr(self.flat.device)
         L.check(L.lib.cg_model_backward(C.byref(self.model), phase, layer, int(bool(accumulate)), st),
@@ -255,3 +259,58 @@ class Engine:
         else:
             t = self.workspace[off: off + B * T * d * 2].view(torch.bfloat16)
         return t.view(B, T, d)
+
+
+class KVCache:
+    """Per-sequence K/V rows of every layer for incremental decoding (cg_model_prefill /
+    cg_model_decode): one prefill of the prompt, then one native call per generated token
+    instead of the reference's full re-forward of the prefix (query_model.py:160-214).
+    Valid while the sequence fits ``Tmax`` <= block_size."""
+
+    def __init__(self, engine: Engine, B: int, Tmax: int):
+        cfg = engine.cfg
+        if Tmax > cfg.block_size:
+            raise ValueError("Tmax exceeds block_size")
+        self.eng, self.B, self.Tmax = engine, int(B), int(Tmax)
+        dev = engine.flat.device
+        nbytes = int(L.lib.cg_kv_cache_bytes(C.byref(engine.model.cfg), self.B, self.Tmax))
+        self.cache = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+        self.seg = torch.zeros(self.B, dtype=torch.int32, device=dev)
+        wsb = int(L.lib.cg_decode_workspace_bytes(C.byref(engine.model.cfg), self.B))
+        self.ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+        self.pos = 0
+
+    @torch.no_grad()
+    def prefill(self, idx: torch.Tensor, window: int | None = None) -> torch.Tensor:
+        """Eval forward of the prompt (B, T); returns fp32 logits (B, T, V)."""
+        eng = self.eng
+        L.require_device(idx, "KVCache.prefill")
+        B, T = idx.shape
+        if B != self.B or T > self.Tmax:
+            raise ValueError(f"prompt {tuple(idx.shape)} does not fit the cache (B={self.B}, Tmax={self.Tmax})")
+        idx = idx.to(torch.int64).contiguous()
+        eng._ensure_workspace(B, T)
+        eng.sync_shadow()
+        logits = torch.empty(B, T, eng.cfg.vocab_size, dtype=torch.float32, device=idx.device)
+        eng._idx, eng._targets = idx, None
+        L.check(L.lib.cg_model_prefill(C.byref(eng.model), idx.data_ptr(), B, T, int(window or 0),
+                                       self.cache.data_ptr(), self.Tmax, self.seg.data_ptr(), logits.data_ptr(),
+                                       L.stream_ptr(idx.device)), "cg_model_prefill")
+        self.pos = T
+        return logits
+
+    @torch.no_grad()
+    def decode(self, tok: torch.Tensor) -> torch.Tensor:
+        """Append one token per sequence (B,) at the current position; returns logits (B, V)."""
+        eng = self.eng
+        if self.pos >= self.Tmax:
+            raise ValueError("KV cache is full (the context reached Tmax)")
+        tok = tok.reshape(self.B).to(device=self.cache.device, dtype=torch.int64).contiguous()
+        eng.sync_shadow()
+        logits = torch.empty(self.B, eng.cfg.vocab_size, dtype=torch.float32, device=tok.device)
+        L.check(L.lib.cg_model_decode(C.byref(eng.model), tok.data_ptr(), self.B, self.pos, self.cache.data_ptr(),
+                                      self.Tmax, self.seg.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                      logits.data_ptr(), L.stream_ptr(tok.device)), "cg_model_decode")
+        self._tok = tok
+        self.pos += 1
+        return logits

@@ -127,17 +127,31 @@ def generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: 
 
 @torch.no_grad()
 def greedy_generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: int,
-                    eos_idx: int | None = None) -> List[int]:
-    """Deterministic argmax continuation (the parity form of ``generate``)."""
+                    eos_idx: int | None = None, kv_cache: bool = True) -> List[int]:
+    """Deterministic argmax continuation (the parity form of ``generate``).  With ``kv_cache``
+    the prompt is prefilled once and each new token costs one cached decode step while the
+    context fits block_size; past it the reference's sliding re-forward takes over."""
     ids = list(ctx_ids)
     max_T = getattr(model, "block_size", None)
+    cache = None
+    logits = None
+    if kv_cache and max_T is not None and 0 < len(ids) < max_T:
+        cache = model.engine.new_kv_cache(1, max_T)
+        logits = cache.prefill(torch.tensor([ids], dtype=torch.long, device=device))[0, -1]
     for _ in range(max_new):
-        next_id = int(torch.argmax(next_token(model, device, ids)).item())
+        if cache is None:
+            logits = next_token(model, device, ids)
+        next_id = int(torch.argmax(logits).item())
         ids.append(next_id)
         if max_T is not None and len(ids) > max_T:
             ids = ids[-max_T:]
         if eos_idx is not None and next_id == eos_idx:
             break
+        if cache is not None:
+            if cache.pos < cache.Tmax:
+                logits = cache.decode(torch.tensor([next_id], device=device))[0]
+            else:  # the context reached block_size: slide and recompute like the reference
+                cache = None
     return ids
 
 

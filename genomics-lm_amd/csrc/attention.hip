@@ -338,3 +338,109 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
   CG_LAUNCH_CHECK();
   return CG_OK;
 }
+
+// ===========================================================================
+// Single-token attention over a KV cache (incremental decoding): the query of position
+// `pos` attends to keys lo..pos of its sequence, lo = its segment start (SEP mask,
+// model_tiny_gpt.py:289-294) raised to pos-window+1 with a local window -- the same keys
+// the full forward's mask row for `pos` admits.  One workgroup per (head, sequence); the
+// scores live in LDS (pos < CG_DECODE_MAX_T).
+// ===========================================================================
+constexpr int DEC_MAXT = 4096;
+template <typename T_>
+__global__ __launch_bounds__(256) void attn_decode_kernel(const T_* __restrict__ q, long long ldq,
+                                                          const T_* __restrict__ cache, long long ldc, int Tmax,
+                                                          int pos, const int32_t* __restrict__ seg, int window, int H,
+                                                          int KV, int hd, float scale, T_* __restrict__ y,
+                                                          long long ldy) {
+  __shared__ float sc[DEC_MAXT];
+  __shared__ float qs[64];
+  __shared__ float red[256];
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int kvh = h / (H / KV);
+  int lo = seg ? seg[b] : 0;
+  if (window > 0) lo = max(lo, pos - window + 1);
+  const int n = pos - lo + 1;
+  if (tid < hd) qs[tid] = ld_act<T_>(q + (long long)b * ldq + (long long)h * hd + tid);
+  __syncthreads();
+  const T_* kb = cache + (long long)b * Tmax * ldc + (long long)kvh * hd;
+  const T_* vb = kb + (long long)KV * hd;
+  float mx = -INFINITY;
+  for (int j = tid; j < n; j += 256) {
+    const T_* kr = kb + (long long)(lo + j) * ldc;
+    float s = 0.f;
+    for (int e = 0; e < hd; ++e) s = fmaf(qs[e], ld_act<T_>(kr + e), s);
+    s *= scale;
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  red[tid] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = fmaxf(red[tid], red[tid + o]);
+    __syncthreads();
+  }
+  const float m = red[0];
+  __syncthreads();
+  float sum = 0.f;
+  for (int j = tid; j < n; j += 256) {
+    const float e = __expf(sc[j] - m);
+    sc[j] = e;
+    sum += e;
+  }
+  red[tid] = sum;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  const float l = red[0];
+  __syncthreads();
+  const int G = 256 / hd;  // key groups per output dim
+  float acc = 0.f;
+  if (tid < G * hd) {
+    const int e = tid % hd, g = tid / hd;
+    for (int j = g; j < n; j += G) acc = fmaf(sc[j], ld_act<T_>(vb + (long long)(lo + j) * ldc + e), acc);
+  }
+  red[tid] = acc;
+  __syncthreads();
+  if (tid < hd) {
+    float o = 0.f;
+    for (int g = 0; g < G; ++g) o += red[g * hd + tid];
+    st_act<T_>(y + (long long)b * ldy + (long long)h * hd + tid, o / l);
+  }
+}
+
+extern "C" int cg_attn_decode(int dtype, const void* q, long long ldq, const void* cache, long long ldc, int Tmax,
+                              int pos, const int32_t* segstate, int window, int B, int H, int KV, int hd, void* y,
+                              long long ldy, void* stream) {
+  if (B <= 0 || H <= 0 || KV <= 0 || H % KV || hd <= 0 || hd > 64 || pos < 0 || pos >= Tmax || pos >= DEC_MAXT)
+    return CG_EINVAL;
+  if (!q || !cache || !y || ldc < 2 * KV * hd) return CG_EINVAL;
+  const float scale = 1.0f / sqrtf((float)hd);
+  const dim3 g(H, B);
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(attn_decode_kernel<bf16_t>, g, dim3(256), 0, (hipStream_t)stream, (const bf16_t*)q, ldq,
+                       (const bf16_t*)cache, ldc, Tmax, pos, segstate, window, H, KV, hd, scale, (bf16_t*)y, ldy);
+  else if (dtype == CG_F32)
+    hipLaunchKernelGGL(attn_decode_kernel<float>, g, dim3(256), 0, (hipStream_t)stream, (const float*)q, ldq,
+                       (const float*)cache, ldc, Tmax, pos, segstate, window, H, KV, hd, scale, (float*)y, ldy);
+  else
+    return CG_EUNSUPPORTED;
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// decoding segment state: seg[b] = pos when the token written at `pos` is the SEP id
+__global__ void segstate_step_kernel(const int64_t* __restrict__ tok, int B, int sep, int pos, int32_t* __restrict__ seg) {
+  const int b = blockIdx.x * 64 + threadIdx.x;
+  if (b < B && tok[b] == sep) seg[b] = pos;
+}
+extern "C" int cg_segstate_step(const int64_t* tok, int B, int sep_id, int pos, int32_t* segstate, void* stream) {
+  if (B <= 0 || sep_id < 0) return CG_OK;
+  if (!tok || !segstate) return CG_EINVAL;
+  hipLaunchKernelGGL(segstate_step_kernel, dim3(cg_cdiv(B, 64)), dim3(64), 0, (hipStream_t)stream, tok, B, sep_id, pos,
+                     segstate);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}

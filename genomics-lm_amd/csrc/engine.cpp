@@ -721,4 +721,158 @@ extern "C" const void* cg_model_hidden(const cg_model* m, int which, int* dtype_
   return nullptr;
 }
 
+// ===========================================================================
+// Incremental decoding (KV cache)
+// ===========================================================================
+extern "C" int cg_attn_decode(int dtype, const void* q, long long ldq, const void* cache, long long ldc, int Tmax,
+                              int pos, const int32_t* segstate, int window, int B, int H, int KV, int hd, void* y,
+                              long long ldy, void* stream);
+extern "C" int cg_segstate_step(const int64_t* tok, int B, int sep_id, int pos, int32_t* segstate, void* stream);
+
+namespace {
+struct DecWS {
+  float *x, *xmid, *mean, *rstd;
+  void *h, *qkv, *y, *a, *g, *gu, *s, *xf;
+};
+size_t carve_dec(const cg_model_cfg* c, const Dims& D, int B, char* base, DecWS& W) {
+  WS w{base, 0};
+  const size_t es = c->dtype == CG_BF16 ? 2 : 4;
+  const int d = D.d;
+  W.x = w.take<float>((size_t)B * d * 4);
+  W.xmid = w.take<float>((size_t)B * d * 4);
+  W.mean = w.take<float>((size_t)B * 4);
+  W.rstd = w.take<float>((size_t)B * 4);
+  W.h = w.take<char>((size_t)B * d * es);
+  W.qkv = w.take<char>((size_t)B * D.Nqkv * es);
+  W.y = w.take<char>((size_t)B * d * es);
+  W.a = W.g = W.gu = W.s = nullptr;
+  if (!D.swiglu) {
+    W.a = w.take<char>((size_t)B * D.hid * es);
+    W.g = w.take<char>((size_t)B * D.hid * es);
+  } else {
+    W.gu = w.take<char>((size_t)B * 2 * D.Hp * es);
+    W.s = w.take<char>((size_t)B * D.Hp * es);
+  }
+  W.xf = w.take<char>((size_t)B * d * es);
+  return w.off + 256;
+}
+// a Ctx whose row count is the B decoding rows (no activation workspace)
+int make_dec_ctx(const cg_model* m, int B, void* stream, Ctx& C) {
+  if (!dims_of(&m->cfg, C.D)) return CG_EINVAL;
+  build_layout(&m->cfg, C.D, C.Lo);
+  C.m = m;
+  C.B = B; C.T = 1; C.M = B;
+  C.dt = m->cfg.dtype;
+  C.s = (hipStream_t)stream;
+  return CG_OK;
+}
+}  // namespace
+
+extern "C" size_t cg_kv_cache_bytes(const cg_model_cfg* cfg, int B, int Tmax) {
+  Dims D;
+  if (!dims_of(cfg, D) || B <= 0 || Tmax <= 0) return 0;
+  const size_t es = cfg->dtype == CG_BF16 ? 2 : 4;
+  return (size_t)D.L * B * Tmax * 2 * D.kvd * es;
+}
+
+extern "C" size_t cg_decode_workspace_bytes(const cg_model_cfg* cfg, int B) {
+  Dims D;
+  if (!dims_of(cfg, D) || B <= 0) return 0;
+  DecWS W;
+  return carve_dec(cfg, D, B, nullptr, W);
+}
+
+extern "C" int cg_model_prefill(cg_model* m, const int64_t* idx, int B, int T, int window, void* cache, int Tmax,
+                                int32_t* segstate, float* logits, void* stream) {
+  if (!m || !idx || !cache || !segstate || B <= 0 || T <= 0 || Tmax < T || Tmax > m->cfg.block_size) return CG_EINVAL;
+  CK(cg_model_forward(m, idx, nullptr, B, T, 0, 0, window, logits, nullptr, stream));
+  Ctx C;
+  CK(make_ctx(m, B, T, stream, C));
+  const Dims& D = C.D;
+  const size_t es = C.dt == CG_BF16 ? 2 : 4;
+  const size_t row = (size_t)2 * D.kvd * es;
+  // the [k|v] columns of each qkv row (post-RoPE K) -> cache rows 0..T-1, one T-row 2-D copy per
+  // (layer, sequence)
+  for (int l = 0; l < D.L; ++l)
+    for (int b = 0; b < B; ++b) {
+      const char* src = (const char*)C.A.la[l].qkv + ((size_t)b * T * D.Nqkv + D.d) * es;
+      char* dst = (char*)cache + ((size_t)l * B + b) * Tmax * row;
+      if (hipMemcpy2DAsync(dst, row, src, (size_t)D.Nqkv * es, row, T, hipMemcpyDeviceToDevice, C.s) != hipSuccess)
+        return CG_ELAUNCH;
+    }
+  if (m->cfg.sep_id >= 0) {
+    if (hipMemcpy2DAsync(segstate, 4, C.A.seg + (T - 1), (size_t)T * 4, 4, B, hipMemcpyDeviceToDevice, C.s) !=
+        hipSuccess)
+      return CG_ELAUNCH;
+  } else if (hipMemsetAsync(segstate, 0, (size_t)B * 4, C.s) != hipSuccess) {
+    return CG_ELAUNCH;
+  }
+  return CG_OK;
+}
+
+extern "C" int cg_model_decode(cg_model* m, const int64_t* tok, int B, int pos, void* cache, int Tmax,
+                               int32_t* segstate, void* dec_ws, size_t dec_ws_bytes, float* logits, void* stream) {
+  if (!m || !tok || !cache || !segstate || !dec_ws || !logits || B <= 0) return CG_EINVAL;
+  if (pos < 0 || pos >= Tmax || Tmax > m->cfg.block_size) return CG_EINVAL;
+  if (m->cfg.dtype == CG_BF16 && !m->shadow) return CG_EINVAL;
+  if (m->cfg.use_rope && (!m->rope_cos || !m->rope_sin)) return CG_EINVAL;
+  Ctx C;
+  CK(make_dec_ctx(m, B, stream, C));
+  const Dims& D = C.D;
+  DecWS W;
+  if (carve_dec(&m->cfg, D, B, nullptr, W) > dec_ws_bytes) return CG_EINVAL;
+  carve_dec(&m->cfg, D, B, (char*)dec_ws, W);
+  const int d = D.d;
+  const float eps = m->cfg.ln_eps > 0 ? m->cfg.ln_eps : 1e-5f;
+  const size_t es = C.dt == CG_BF16 ? 2 : 4;
+  const size_t row = (size_t)2 * D.kvd * es;
+  CK(cg_embed_fwd(tok, P(C, C.Lo.tok), C.Lo.pos >= 0 ? P(C, C.Lo.pos) + (size_t)pos * d : nullptr, W.x, B, 1, d, 0,
+                  0.f, C.s));
+  CK(cg_segstate_step(tok, B, m->cfg.sep_id, pos, segstate, C.s));
+  for (int l = 0; l < D.L; ++l) {
+    const auto& o = C.Lo.lay[l];
+    CK(cg_layernorm_fwd(C.dt, W.x, d, P(C, o.ln1w), P(C, o.ln1b), W.h, d, W.mean, W.rstd, B, d, eps, C.s));
+    cg_gemm_desc g = lin_fwd(C, W.h, d, o.wqkv, d, D.Nqkv, d, W.qkv, D.Nqkv);
+    g.epilogue = CG_EPI_BIAS; g.bias = P(C, o.bqkv);
+    CK(cg_gemm(&g, C.s));
+    if (D.rope)
+      CK(cg_rope_tab(C.dt, W.qkv, D.Nqkv, B, 1, D.H, D.KV, D.hd, m->rope_cos + (size_t)pos * (D.hd / 2),
+                     m->rope_sin + (size_t)pos * (D.hd / 2), 0, C.s));
+    char* cl = (char*)cache + (size_t)l * B * Tmax * row;
+    if (hipMemcpy2DAsync(cl + (size_t)pos * row, (size_t)Tmax * row, (const char*)W.qkv + (size_t)d * es,
+                         (size_t)D.Nqkv * es, row, B, hipMemcpyDeviceToDevice, C.s) != hipSuccess)
+      return CG_ELAUNCH;
+    CK(cg_attn_decode(C.dt, W.qkv, D.Nqkv, cl, 2 * D.kvd, Tmax, pos, m->cfg.sep_id >= 0 ? segstate : nullptr,
+                      m->window, B, D.H, D.KV, D.hd, W.y, d, C.s));
+    g = lin_fwd(C, W.y, d, o.wp, d, d, d, W.xmid, d);
+    g.c_dtype = CG_F32;
+    g.epilogue = CG_EPI_BIAS | CG_EPI_RESID; g.bias = P(C, o.bp); g.resid = W.x; g.ldr = d;
+    CK(cg_gemm(&g, C.s));
+    CK(cg_layernorm_fwd(C.dt, W.xmid, d, P(C, o.ln2w), P(C, o.ln2b), W.h, d, W.mean, W.rstd, B, d, eps, C.s));
+    if (!D.swiglu) {
+      g = lin_fwd(C, W.h, d, o.w1, d, D.hid, d, W.g, D.hid);
+      g.epilogue = CG_EPI_BIAS | CG_EPI_GELU; g.bias = P(C, o.b1); g.aux_out = W.a; g.ld_aux = D.hid;
+      CK(cg_gemm(&g, C.s));
+      g = lin_fwd(C, W.g, D.hid, o.w2, D.hid, d, D.hid, W.x, d);
+      g.c_dtype = CG_F32;
+      g.epilogue = CG_EPI_BIAS | CG_EPI_RESID; g.bias = P(C, o.b2); g.resid = W.xmid; g.ldr = d;
+      CK(cg_gemm(&g, C.s));
+    } else {
+      g = lin_fwd(C, W.h, d, o.wgu, d, 2 * D.Hp, d, W.gu, 2 * D.Hp);
+      CK(cg_gemm(&g, C.s));
+      CK(cg_swiglu_fwd(C.dt, W.gu, 2 * D.Hp, D.Hp, W.s, D.Hp, B, D.hid, C.s));
+      g = lin_fwd(C, W.s, D.Hp, o.wd, D.Hp, d, D.Hp, W.x, d);
+      g.c_dtype = CG_F32;
+      g.epilogue = CG_EPI_RESID; g.resid = W.xmid; g.ldr = d;
+      CK(cg_gemm(&g, C.s));
+    }
+  }
+  CK(cg_layernorm_fwd(C.dt, W.x, d, P(C, C.Lo.lnfw), P(C, C.Lo.lnfb), W.xf, d, W.mean, W.rstd, B, d, eps, C.s));
+  const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+  cg_gemm_desc g = lin_fwd(C, W.xf, d, hoff, d, D.V, d, logits, D.V);
+  g.c_dtype = CG_F32;
+  CK(cg_gemm(&g, C.s));
+  return CG_OK;
+}
+
 extern "C" const char* cg_version(void) { return "codonlm_hip 0.1 gfx950"; }

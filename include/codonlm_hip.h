@@ -297,6 +297,29 @@ int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* s
  * L+1 = ln_f output) inside the workspace after a forward; dtype in *dtype_out */
 const void* cg_model_hidden(const cg_model* m, int which, int* dtype_out, long long* ld);
 
+/* Incremental decoding with a KV cache (query_model.py generate / next_token :160-214 without
+ * re-running the whole prefix).  The cache holds, per layer and sequence, the post-RoPE K and
+ * V rows of every position: layout [L][B][Tmax][2*kv_dim] in the model dtype.  Valid while
+ * the context fits block_size (the reference then slides its window and recomputes).
+ *   cg_model_prefill: full eval forward of idx [B][T] (logits [B*T][V]), fills cache rows
+ *     0..T-1 and segstate[b] (start of the last SEP segment; 0 without sep masking).
+ *   cg_model_decode: one new token per sequence at position pos (= current length): writes
+ *     its cache rows and logits [B][V].  dec_ws: cg_decode_workspace_bytes(cfg, B). */
+size_t cg_kv_cache_bytes(const cg_model_cfg* cfg, int B, int Tmax);
+size_t cg_decode_workspace_bytes(const cg_model_cfg* cfg, int B);
+int cg_model_prefill(cg_model* m, const int64_t* idx, int B, int T, int window, void* cache, int Tmax,
+                     int32_t* segstate, float* logits, void* stream);
+int cg_model_decode(cg_model* m, const int64_t* tok, int B, int pos, void* cache, int Tmax,
+                    int32_t* segstate, void* dec_ws, size_t dec_ws_bytes, float* logits, void* stream);
+/* the decode step's attention: query rows q [B][ldq] (head h at column h*hd), cache rows of
+ * one layer [B][Tmax][ldc] (K at kv_head*hd, V at KV*hd + kv_head*hd), keys
+ * max(segstate[b], pos-window+1) .. pos; y [B][ldy] */
+int cg_attn_decode(int dtype, const void* q, long long ldq, const void* cache, long long ldc, int Tmax,
+                   int pos, const int32_t* segstate, int window, int B, int H, int KV, int hd, void* y,
+                   long long ldy, void* stream);
+/* segstate[b] = pos where tok[b] == sep_id (the SEP token opens its segment) */
+int cg_segstate_step(const int64_t* tok, int B, int sep_id, int pos, int32_t* segstate, void* stream);
+
 /* Live probe of one kernel class during a real run: HIP events are recorded on the
  * launching stream around each launch of the selected kernel together with its
  * algorithmic work (FLOPs for MFMA kernels).  kind 0 disables.  cg_probe_read
