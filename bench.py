@@ -32,6 +32,10 @@ CONFIGS = {
     "c4": dict(n_layer=12, n_head=8, n_embd=512, block_size=1024, batch=16, swiglu=False, rope=False, kv=None),
     "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, batch=64, swiglu=False, rope=False, kv=None),
     "c3": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=64, swiglu=True, rope=True, kv=4),
+    # stage2.6_large_scaling + termination head + multi-offset heads: the trainer's
+    # full objective (loop.py:1075-1112) on packed BOS..EOS,SEP segments
+    "c5": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=32, swiglu=False, rope=False, kv=None,
+               offsets=(2, 4, 8, 16, 32), term=True),
 }
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
@@ -44,6 +48,7 @@ def flops_per_token(c, V=68):
     hid = int(8 * d // 3) if c["swiglu"] else 4 * d
     mlp = 3 * d * hid if c["swiglu"] else 2 * d * hid
     n_mm = L * (d * (d + 2 * kvd) + d * d + mlp) + d * V
+    n_mm += (5 * d if c.get("term") else 0) + len(c.get("offsets", ())) * (2 * d * d + d * V)  # aux heads
     # 6*N_mm + 6*L*d*T (causal-exact attention, no recompute)
     return 6 * n_mm + 6 * L * d * T
 
@@ -116,8 +121,10 @@ def main():
     B = args.batch or c["batch"]
     T = c["block_size"]
     torch.manual_seed(1337)
+    aux = bool(c.get("offsets") or c.get("term"))
     model = TinyGPT(68, T, n_layer=c["n_layer"], n_head=c["n_head"], n_embd=c["n_embd"], dropout=0.1,
                     label_smoothing=0.05, n_kv_head=c["kv"], use_swiglu=c["swiglu"], use_rope=c["rope"],
+                    termination_aux=bool(c.get("term")), multi_offset_targets=list(c.get("offsets", ())) or None,
                     compute_dtype=args.dtype, device=dev)
     if world > 1:  # identical replicas
         dist.broadcast(model.flat_parameters(), 0)
@@ -137,6 +144,35 @@ def main():
     def run(i):
         xb, yb = batches[i % nbuf]
         return stepper.step(xb, yb, seed=1000 + i)
+
+    if aux:  # the trainer's objective through the model API (aux heads + objectives.py mirror)
+        from codonlm_amd.training import objectives as obj
+        offw = {k: 1.0 / len(c["offsets"]) for k in c.get("offsets", ())}
+        for j, (xb, yb) in enumerate(batches):  # packed segments: BOS ... EOS, SEP every ~330 tokens
+            tok = torch.cat([xb[:, :1], yb], 1)
+            tok[:, 0] = 1
+            for p0 in range(330 + j, T, 330):
+                tok[:, p0 - 1], tok[:, p0] = 2, 3
+                if p0 + 1 <= T:
+                    tok[:, p0 + 1] = 1
+            batches[j] = (tok[:, :-1].contiguous(), tok[:, 1:].contiguous())
+
+        def run(i):  # noqa: F811
+            xb, yb = batches[i % nbuf]
+            opt.zero_grad()
+            _, loss, auxo = model(xb, yb, return_aux=True)
+            total = loss
+            if offw:
+                off_total, _ = obj.multi_offset_lm_loss(auxo["offset_logits"], yb, offw, label_smoothing=0.05)
+                total = total + off_total
+            if c.get("term"):
+                labels = obj.termination_distance_bucket_labels(yb, stop_ids=(2,))
+                total = total + 0.1 * obj.termination_aux_loss(auxo["termination_logits"], labels)
+            total.backward()
+            if world > 1:
+                dist.all_reduce(model.flat_grads())
+            opt.step(grad_scale=1.0 / world)
+            return total
 
     for i in range(args.warmup):
         loss = run(i)

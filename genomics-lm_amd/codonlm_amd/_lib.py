@@ -119,7 +119,7 @@ SIGNATURES = {
     "cg_model_param_layout": (i32, [C.POINTER(ModelCfg), C.POINTER(ParamEntry), i32, C.POINTER(i64)]),
     "cg_model_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
     "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
-    "cg_model_aux_forward": (i32, [C.POINTER(Model), vp, i64, C.POINTER(vp), vp]),
+    "cg_model_aux_forward": (i32, [C.POINTER(Model), vp, i64, C.POINTER(vp), i64, vp]),
     "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),
     "cg_kv_cache_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
     "cg_decode_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32]),

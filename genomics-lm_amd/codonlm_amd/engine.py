@@ -195,12 +195,15 @@ class Engine:
         term = None
         if cfg.termination_aux:
             term = torch.empty(M, cfg.termination_n_classes, dtype=torch.float32, device=dev)
-        offs = [torch.empty(M, cfg.vocab_size, dtype=torch.float32, device=dev) for _ in cfg.multi_offset_targets]
+        # rows padded to a multiple of 16 columns (the GEMM then takes the vector tiles); the
+        # callers see [:, :V] views
+        Vp = (cfg.vocab_size + 15) // 16 * 16
+        offs = [torch.empty(M, Vp, dtype=torch.float32, device=dev) for _ in cfg.multi_offset_targets]
         arr = (C.c_void_p * len(offs))(*[o.data_ptr() for o in offs]) if offs else None
         L.check(L.lib.cg_model_aux_forward(C.byref(self.model), term.data_ptr() if term is not None else None,
-                                           term.stride(0) if term is not None else 0, arr, L.stream_ptr(dev)),
+                                           term.stride(0) if term is not None else 0, arr, Vp, L.stream_ptr(dev)),
                 "cg_model_aux_forward")
-        return term, offs
+        return term, [o[:, :cfg.vocab_size] for o in offs]
 
     def set_head_grads(self, scale: float, d_term=None, d_offsets=None):
         """Gradients phase 0 consumes: the next-codon loss scale and the aux-head logit

@@ -554,12 +554,12 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
 }
 
 extern "C" int cg_model_aux_forward(cg_model* m, float* term_logits, long long ld_term, float* const* offset_logits,
-                                    void* stream) {
+                                    long long ld_off, void* stream) {
   if (!m || !m->idx || m->B <= 0 || m->T <= 0) return CG_EINVAL;
   const int nc = m->cfg.termination_aux ? m->cfg.termination_n_classes : 0;
   const int noff = std::min(m->cfg.n_offsets, 8);
   if (nc > 0 && (!term_logits || ld_term < nc)) return CG_EINVAL;
-  if (noff > 0 && !offset_logits) return CG_EINVAL;
+  if (noff > 0 && (!offset_logits || ld_off < m->cfg.vocab_size)) return CG_EINVAL;
   for (int i = 0; i < noff; ++i)
     if (!offset_logits[i]) return CG_EINVAL;
   Ctx C;
@@ -583,7 +583,7 @@ extern "C" int cg_model_aux_forward(cg_model* m, float* term_logits, long long l
     g = lin_fwd(C, A.og[i], d, C.Lo.off2w[i], d, d, d, A.opj[i], d);
     g.epilogue = CG_EPI_BIAS; g.bias = P(C, C.Lo.off2b[i]);
     CK(cg_gemm(&g, C.s));
-    g = lin_fwd(C, A.opj[i], d, hoff, d, D.V, d, offset_logits[i], D.V);
+    g = lin_fwd(C, A.opj[i], d, hoff, d, ld_off >= D.Vp ? D.Vp : D.V, d, offset_logits[i], ld_off);
     g.c_dtype = CG_F32;
     CK(cg_gemm(&g, C.s));
   }

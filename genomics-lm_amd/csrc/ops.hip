@@ -1246,36 +1246,51 @@ extern "C" int cg_offset_targets(const int64_t* y, int B, int T, int offset, con
   return CG_OK;
 }
 // termination_distance_bucket_labels (objectives.py:63-91): distance to the next stop id at or
-// after t, bucketed as #(edges < distance); no later stop -> n_edges; PAD -> ignore_index
-__global__ __launch_bounds__(256) void termination_labels_kernel(const int64_t* __restrict__ y, int B, int T,
-                                                                 IdSet stops, IdSet edges, int ignore,
-                                                                 int64_t* __restrict__ lab) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= (long long)B * T) return;
-  const long long b = i / T;
-  const int t = (int)(i - b * T);
+// after t, bucketed as #(edges < distance); no later stop -> n_edges; PAD -> ignore_index.
+// One workgroup per row: each thread owns a contiguous chunk, a suffix-min over the chunks'
+// first stop positions gives every chunk its next stop, then a reverse sweep inside the chunk.
+__global__ __launch_bounds__(256) void termination_labels_kernel(const int64_t* __restrict__ y, int T, IdSet stops,
+                                                                 IdSet edges, int ignore, int64_t* __restrict__ lab) {
+  __shared__ int sfx[257];
+  const int tid = threadIdx.x;
+  const long long b = blockIdx.x;
   const int64_t* row = y + b * T;
-  int64_t out;
-  if (row[t] == 0) {
-    out = ignore;
-  } else {
-    int nxt = T;
-    for (int s = t; s < T; ++s)
-      if (in_set(stops, row[s])) {
-        nxt = s;
-        break;
-      }
-    if (nxt == T) {
-      out = edges.n;
+  int64_t* out = lab + b * T;
+  const int per = (T + 255) / 256;
+  const int t0 = min(T, tid * per), t1 = min(T, t0 + per);
+  int first = T;
+  for (int t = t0; t < t1; ++t)
+    if (in_set(stops, row[t])) {
+      first = t;
+      break;
+    }
+  sfx[tid] = first;
+  if (tid == 0) sfx[256] = T;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive suffix minimum
+    const int v = tid + o < 256 ? sfx[tid + o] : T;
+    __syncthreads();
+    sfx[tid] = min(sfx[tid], v);
+    __syncthreads();
+  }
+  int nxt = sfx[tid + 1];
+  for (int t = t1 - 1; t >= t0; --t) {
+    const int64_t v = row[t];
+    if (in_set(stops, v)) nxt = t;
+    int64_t o;
+    if (v == 0) {
+      o = ignore;
+    } else if (nxt == T) {
+      o = edges.n;
     } else {
       const int dist = nxt - t;
       int c = 0;
 #pragma unroll
       for (int e = 0; e < 8; ++e) c += (e < edges.n) && (dist > edges.id[e]);
-      out = c;
+      o = c;
     }
+    out[t] = o;
   }
-  lab[i] = out;
 }
 extern "C" int cg_termination_labels(const int64_t* y, int B, int T, const int* stop_ids, int n_stop, const int* edges,
                                      int n_edges, int ignore_index, int64_t* labels, void* stream) {
@@ -1287,8 +1302,8 @@ extern "C" int cg_termination_labels(const int64_t* y, int B, int T, const int* 
   const long long total = (long long)B * T;
   if (total == 0) return CG_OK;
   if (!y || !labels) return CG_EINVAL;
-  hipLaunchKernelGGL(termination_labels_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, y, B, T, st, ed, ignore_index, labels);
+  hipLaunchKernelGGL(termination_labels_kernel, dim3((unsigned)B), dim3(256), 0, (hipStream_t)stream, y, T, st, ed,
+                     ignore_index, labels);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }

@@ -282,10 +282,12 @@ int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, in
                      void* stream);
 /* auxiliary heads on the ln_f output of the last forward (model_tiny_gpt.py:329-337):
  * termination logits fp32 [B*T][ld_term] = xf W_t^T + b_t (termination_aux), and per
- * offset head i: logits_i fp32 [B*T][V] = head(W2 gelu(W1 xf + b1) + b2) (tied head).
+ * offset head i: logits_i fp32 [B*T][ld_off] = head(W2 gelu(W1 xf + b1) + b2) (tied head);
+ * ld_off >= V; with ld_off >= round_up(V, 16) the zero pad columns are computed too (the
+ * product then takes the vector / persistent GEMM tiles).
  * The offset activations stay in the workspace for the backward. */
 int cg_model_aux_forward(cg_model* m, float* term_logits, long long ld_term,
-                         float* const* offset_logits, void* stream);
+                         float* const* offset_logits, long long ld_off, void* stream);
 /* backward in phases so the caller can overlap per-bucket gradient all-reduce:
  *   phase 0: head (+ aux heads) + ln_f; phase 1: one block `layer` (call L-1 .. 0);
  *   phase 2: embeddings.  Phase 0 scales the next-codon head gradient by head_grad_scale
