@@ -129,6 +129,7 @@ SIGNATURES = {
     "cg_segstate_step": (i32, [vp, i32, i32, i32, vp, vp]),
     "cg_model_hidden": (vp, [C.POINTER(Model), i32, C.POINTER(i32), C.POINTER(i64)]),
     "cg_probe_enable": (i32, [i32]),
+    "cg_probe_sample": (i32, [i32]),
     "cg_probe_read": (i32, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)]),
     "cg_version": (C.c_char_p, []),
 }

@@ -15,6 +15,9 @@ struct Probe {
   size_t used = 0;
   double work = 0.0;
   long long launches = 0;
+  long long seen = 0;   // launches of the selected kernel since enable
+  int every = 1;        // record 1 of every `every` launches (sampling keeps the event cost low)
+  bool open = false;    // the current launch is being recorded
   std::mutex mu;
 } g_probe;
 }  // namespace
@@ -24,10 +27,15 @@ int cg_probe_kind() { return g_probe.kind; }
 void cg_probe_begin(int kind, hipStream_t s) {
   if (g_probe.kind != kind) return;
   std::lock_guard<std::mutex> lk(g_probe.mu);
+  g_probe.open = (g_probe.seen++ % g_probe.every) == 0;
+  if (!g_probe.open) return;
   if (g_probe.used + 2 > g_probe.pool.size()) {
     for (int i = 0; i < 64; ++i) {
       hipEvent_t e;
-      if (hipEventCreate(&e) != hipSuccess) return;
+      if (hipEventCreate(&e) != hipSuccess) {
+        g_probe.open = false;
+        return;
+      }
       g_probe.pool.push_back(e);
     }
   }
@@ -37,6 +45,8 @@ void cg_probe_begin(int kind, hipStream_t s) {
 void cg_probe_end(int kind, hipStream_t s, double work) {
   if (g_probe.kind != kind) return;
   std::lock_guard<std::mutex> lk(g_probe.mu);
+  if (!g_probe.open) return;
+  g_probe.open = false;
   (void)hipEventRecord(g_probe.pool[g_probe.used + 1], s);
   g_probe.used += 2;
   g_probe.work += work;
@@ -49,6 +59,15 @@ extern "C" int cg_probe_enable(int kind) {
   g_probe.used = 0;
   g_probe.work = 0.0;
   g_probe.launches = 0;
+  g_probe.seen = 0;
+  g_probe.open = false;
+  return CG_OK;
+}
+
+extern "C" int cg_probe_sample(int every) {
+  if (every < 1) return CG_EINVAL;
+  std::lock_guard<std::mutex> lk(g_probe.mu);
+  g_probe.every = every;
   return CG_OK;
 }
 

@@ -336,6 +336,9 @@ enum {
   CG_PROBE_ATTN_DKDV = 6     /* attn_bwd_dkdv_mfma                                 */
 };
 int cg_probe_enable(int kind);
+/* record 1 of every `every` launches of the probed kernel (default 1 = all); the launch
+ * count and work returned by cg_probe_read cover the recorded launches only */
+int cg_probe_sample(int every);
 int cg_probe_read(double* work, double* ms, long long* launches);
 
 const char* cg_version(void);
