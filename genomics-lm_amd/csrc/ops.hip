@@ -51,49 +51,86 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
-// Vectorised fast path: cols = 128*V2, each lane owns V2 float2 pairs at columns
-// 2*(lane + 64 i) (every wave-instruction moves 512 contiguous bytes).
-__device__ __forceinline__ void st2(float* p, float a, float b) { *(float2*)p = make_float2(a, b); }
-__device__ __forceinline__ void st2(bf16_t* p, float a, float b) {
-  *(uint32_t*)p = (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+// Vectorised fast path: cols = 64*W*NV, each lane owns NV runs of W consecutive columns at
+// W*(lane + 64 i) (every wave-instruction moves 64*W contiguous elements; W = 4 -> 1 KiB of
+// fp32 x per wave-instruction, W = 2 for widths that are not a multiple of 256).
+template <int W>
+__device__ __forceinline__ void ldw(const float* p, float* v) {
+  if constexpr (W == 4) {
+    const float4 a = *(const float4*)p;
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  } else {
+    const float2 a = *(const float2*)p;
+    v[0] = a.x; v[1] = a.y;
+  }
 }
-__device__ __forceinline__ float2 ld2(const float* p) { return *(const float2*)p; }
-__device__ __forceinline__ float2 ld2(const bf16_t* p) {
-  const uint32_t u = *(const uint32_t*)p;
-  return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u));
+template <int W>
+__device__ __forceinline__ void ldw(const bf16_t* p, float* v) {
+  uint32_t u[W / 2];
+  if constexpr (W == 4) {
+    const uint2 t = *(const uint2*)p;
+    u[0] = t.x; u[1] = t.y;
+  } else {
+    u[0] = *(const uint32_t*)p;
+  }
+#pragma unroll
+  for (int j = 0; j < W / 2; ++j) {
+    v[2 * j] = __uint_as_float(u[j] << 16);
+    v[2 * j + 1] = __uint_as_float(u[j] & 0xFFFF0000u);
+  }
+}
+template <int W>
+__device__ __forceinline__ void stw(float* p, const float* v) {
+  if constexpr (W == 4) *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  else *(float2*)p = make_float2(v[0], v[1]);
+}
+template <int W>
+__device__ __forceinline__ void stw(bf16_t* p, const float* v) {
+  uint32_t u[W / 2];
+#pragma unroll
+  for (int j = 0; j < W / 2; ++j) u[j] = (uint32_t)f2bf(v[2 * j]) | ((uint32_t)f2bf(v[2 * j + 1]) << 16);
+  if constexpr (W == 4) *(uint2*)p = make_uint2(u[0], u[1]);
+  else *(uint32_t*)p = u[0];
 }
 
-template <typename TO, int V2>
+template <typename TO, int W, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, long long ldx,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
                                                   TO* __restrict__ y, long long ldy, float* __restrict__ mean,
                                                   float* __restrict__ rstd, int rows, float eps) {
-  constexpr int cols = 128 * V2;
+  constexpr int cols = 64 * W * NV;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const float* xr = x + (long long)row * ldx;
-  float2 v[V2];
+  float v[NV][W];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < V2; ++i) {
-    v[i] = ld2(xr + 2 * (lane + 64 * i));
-    s += v[i].x + v[i].y;
+  for (int i = 0; i < NV; ++i) {
+    ldw<W>(xr + W * (lane + 64 * i), v[i]);
+#pragma unroll
+    for (int j = 0; j < W; ++j) s += v[i][j];
   }
   const float mu = wave_sum(s) * (1.0f / cols);
   float q = 0.f;
 #pragma unroll
-  for (int i = 0; i < V2; ++i) {
-    const float a = v[i].x - mu, b = v[i].y - mu;
-    q += a * a + b * b;
-  }
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const float a = v[i][j] - mu;
+      q += a * a;
+    }
   const float rs = rsqrtf(wave_sum(q) * (1.0f / cols) + eps);
   TO* yr = y + (long long)row * ldy;
 #pragma unroll
-  for (int i = 0; i < V2; ++i) {
-    const int c = 2 * (lane + 64 * i);
-    const float2 gm = *(const float2*)(gamma + c), bt = *(const float2*)(beta + c);
-    st2(yr + c, (v[i].x - mu) * rs * gm.x + bt.x, (v[i].y - mu) * rs * gm.y + bt.y);
+  for (int i = 0; i < NV; ++i) {
+    const int c = W * (lane + 64 * i);
+    float gm[W], bt[W], o[W];
+    ldw<W>(gamma + c, gm);
+    ldw<W>(beta + c, bt);
+#pragma unroll
+    for (int j = 0; j < W; ++j) o[j] = (v[i][j] - mu) * rs * gm[j] + bt[j];
+    stw<W>(yr + c, o);
   }
   if (lane == 0) {
     if (mean) mean[row] = mu;
@@ -101,11 +138,27 @@ __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, l
   }
 }
 
+// W = 4 when cols is a multiple of 256 and every row start is 16-B aligned, else W = 2
+static inline int ln_width(int cols, const void* a, long long lda, const void* b, long long ldb, int b_bytes) {
+  if (cols % 256 == 0 && cols <= 1024 && lda % 4 == 0 && ldb % 4 == 0 && ((uintptr_t)a & 15) == 0 &&
+      ((uintptr_t)b & (4 * b_bytes - 1)) == 0)
+    return 4;
+  if (cols % 128 == 0 && cols <= 1024 && lda % 2 == 0 && ldb % 2 == 0) return 2;
+  return 0;
+}
+
 template <typename TO>
-static bool ln_fwd_fast(int V2, dim3 g, hipStream_t s, const float* x, long long ldx, const float* gamma,
+static bool ln_fwd_fast(int W, int cols, dim3 g, hipStream_t s, const float* x, long long ldx, const float* gamma,
                         const float* beta, TO* y, long long ldy, float* mean, float* rstd, int rows, float eps) {
-#define LNF(N) case N: hipLaunchKernelGGL((ln_fwd_vec<TO, N>), g, dim3(256), 0, s, x, ldx, gamma, beta, y, ldy, mean, rstd, rows, eps); return true;
-  switch (V2) { LNF(1) LNF(2) LNF(3) LNF(4) LNF(6) LNF(8) default: return false; }
+#define LNF(WW, N) \
+  case N: hipLaunchKernelGGL((ln_fwd_vec<TO, WW, N>), g, dim3(256), 0, s, x, ldx, gamma, beta, y, ldy, mean, rstd, rows, eps); return true;
+  if (W == 4) {
+    switch (cols / 256) { LNF(4, 1) LNF(4, 2) LNF(4, 3) LNF(4, 4) default: return false; }
+  }
+  if (W == 2) {
+    switch (cols / 128) { LNF(2, 1) LNF(2, 2) LNF(2, 3) LNF(2, 4) LNF(2, 6) LNF(2, 8) default: return false; }
+  }
+  return false;
 #undef LNF
 }
 
@@ -115,11 +168,12 @@ extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, co
   if (cols <= 0 || cols > 64 * LN_MAXV || rows < 0) return CG_EUNSUPPORTED;
   if (rows == 0) return CG_OK;
   dim3 g(cg_cdiv(rows, 4));
-  if (cols % 128 == 0 && (ldx % 2) == 0 && (ldy % 2) == 0) {
+  const int W = ln_width(cols, x, ldx, y, ldy, out_dtype == CG_BF16 ? 2 : 4);
+  if (W) {
     const bool ok = out_dtype == CG_BF16
-                        ? ln_fwd_fast<bf16_t>(cols / 128, g, (hipStream_t)stream, x, ldx, gamma, beta, (bf16_t*)y,
+                        ? ln_fwd_fast<bf16_t>(W, cols, g, (hipStream_t)stream, x, ldx, gamma, beta, (bf16_t*)y,
                                               ldy, mean, rstd, rows, eps)
-                        : ln_fwd_fast<float>(cols / 128, g, (hipStream_t)stream, x, ldx, gamma, beta, (float*)y, ldy,
+                        : ln_fwd_fast<float>(W, cols, g, (hipStream_t)stream, x, ldx, gamma, beta, (float*)y, ldy,
                                              mean, rstd, rows, eps);
     if (ok) {
       CG_LAUNCH_CHECK();
@@ -143,117 +197,147 @@ extern "C" int cg_layernorm_bwd_blocks(int rows) {
   return b > 1024 ? 1024 : (b < 1 ? 1 : b);
 }
 
-// Vectorised backward: cols = 128*V2; one wave per row, per-lane dgamma/dbeta partials in
-// registers, combined across the block's 4 waves in LDS (fixed order).
-template <typename TD, typename TO, int V2>
+// Vectorised backward: cols = 64*W*NV (runs as in ln_fwd_vec); one wave per row, per-lane
+// dgamma/dbeta partials in registers, combined across the block's 4 waves in LDS (fixed order).
+template <typename TD, typename TO, int W, int NV>
 __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, long long lddy, const float* __restrict__ x,
                                                   long long ldx, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, const float* __restrict__ gamma,
                                                   const float* __restrict__ g_in, float* __restrict__ g_out,
                                                   TO* __restrict__ g_out_t, uint32_t seed, uint32_t thr, float dscale,
                                                   float* __restrict__ partials, int rows, int want_col) {
-  constexpr int cols = 128 * V2;
-  __shared__ float2 red[4][3 * 64 * V2];
+  constexpr int cols = 64 * W * NV;
+  __shared__ __attribute__((aligned(16))) float red[4][3 * cols];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int per = (rows + gridDim.x - 1) / gridDim.x;
   const int r_begin = blockIdx.x * per, r_end = min(rows, r_begin + per);
-  float2 gm[V2], dg[V2], db[V2], dc[V2];
+  float gm[NV][W], dg[NV][W], db[NV][W], dc[NV][W];
 #pragma unroll
-  for (int i = 0; i < V2; ++i) {
-    gm[i] = *(const float2*)(gamma + 2 * (lane + 64 * i));
-    dg[i] = make_float2(0.f, 0.f);
-    db[i] = make_float2(0.f, 0.f);
-    dc[i] = make_float2(0.f, 0.f);
+  for (int i = 0; i < NV; ++i) {
+    ldw<W>(gamma + W * (lane + 64 * i), gm[i]);
+#pragma unroll
+    for (int j = 0; j < W; ++j) dg[i][j] = db[i][j] = dc[i][j] = 0.f;
   }
   for (int row = r_begin + wave; row < r_end; row += 4) {
     const float mu = mean[row], rs = rstd[row];
     const float* xr = x + (long long)row * ldx;
     const TD* dyr = dy + (long long)row * lddy;
-    float2 xh[V2], gy[V2];
+    float xh[NV][W], gy[NV][W];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < V2; ++i) {
-      const int c = 2 * (lane + 64 * i);
-      const float2 d = ld2(dyr + c), xv = ld2(xr + c);
-      xh[i] = make_float2((xv.x - mu) * rs, (xv.y - mu) * rs);
-      gy[i] = make_float2(d.x * gm[i].x, d.y * gm[i].y);
-      dg[i].x += d.x * xh[i].x; dg[i].y += d.y * xh[i].y;
-      db[i].x += d.x; db[i].y += d.y;
-      s1 += gy[i].x + gy[i].y;
-      s2 += gy[i].x * xh[i].x + gy[i].y * xh[i].y;
+    for (int i = 0; i < NV; ++i) {
+      const int c = W * (lane + 64 * i);
+      float d[W], xv[W];
+      ldw<W>(dyr + c, d);
+      ldw<W>(xr + c, xv);
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        xh[i][j] = (xv[j] - mu) * rs;
+        gy[i][j] = d[j] * gm[i][j];
+        dg[i][j] += d[j] * xh[i][j];
+        db[i][j] += d[j];
+        s1 += gy[i][j];
+        s2 += gy[i][j] * xh[i][j];
+      }
     }
     s1 = wave_sum(s1) * (1.0f / cols);
     s2 = wave_sum(s2) * (1.0f / cols);
     float* go = g_out + (long long)row * cols;
     const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
 #pragma unroll
-    for (int i = 0; i < V2; ++i) {
-      const int c = 2 * (lane + 64 * i);
-      float a = rs * (gy[i].x - s1 - xh[i].x * s2), b = rs * (gy[i].y - s1 - xh[i].y * s2);
+    for (int i = 0; i < NV; ++i) {
+      const int c = W * (lane + 64 * i);
+      float o[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) o[j] = rs * (gy[i][j] - s1 - xh[i][j] * s2);
       if (gi) {
-        const float2 g2 = ld2(gi + c);
-        a += g2.x; b += g2.y;
+        float g2[W];
+        ldw<W>(gi + c, g2);
+#pragma unroll
+        for (int j = 0; j < W; ++j) o[j] += g2[j];
       }
-      st2(go + c, a, b);
+      stw<W>(go + c, o);
       if (g_out_t) {
         if (thr) {
-          const uint32_t h = cg_hash_pair(seed, (uint32_t)row, (uint32_t)c >> 1);
-          a = (h & 0xFFFFu) >= thr ? a * dscale : 0.f;
-          b = (h >> 16) >= thr ? b * dscale : 0.f;
+#pragma unroll
+          for (int j = 0; j < W; j += 2) {
+            const uint32_t h = cg_hash_pair(seed, (uint32_t)row, (uint32_t)(c + j) >> 1);
+            o[j] = (h & 0xFFFFu) >= thr ? o[j] * dscale : 0.f;
+            o[j + 1] = (h >> 16) >= thr ? o[j + 1] * dscale : 0.f;
+          }
         }
-        st2(g_out_t + (long long)row * cols + c, a, b);
-        dc[i].x += a; dc[i].y += b;  // column sum of the consumer's dY (its bias gradient)
+        stw<W>(g_out_t + (long long)row * cols + c, o);
+#pragma unroll
+        for (int j = 0; j < W; ++j) dc[i][j] += o[j];  // column sum of the consumer's dY (its bias gradient)
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < V2; ++i) {
-    red[wave][lane + 64 * i] = dg[i];
-    red[wave][64 * V2 + lane + 64 * i] = db[i];
-    red[wave][128 * V2 + lane + 64 * i] = dc[i];
+  for (int i = 0; i < NV; ++i) {
+    const int c = W * (lane + 64 * i);
+    stw<W>(&red[wave][c], dg[i]);
+    stw<W>(&red[wave][cols + c], db[i]);
+    stw<W>(&red[wave][2 * cols + c], dc[i]);
   }
   __syncthreads();
   const int nw = (want_col ? 3 : 2);
-  for (int e = threadIdx.x; e < nw * 64 * V2; e += 256) {
-    const float2 s = make_float2(red[0][e].x + red[1][e].x + red[2][e].x + red[3][e].x,
-                                 red[0][e].y + red[1][e].y + red[2][e].y + red[3][e].y);
-    const int which = e / (64 * V2), rem = e % (64 * V2);
-    *(float2*)(partials + (long long)blockIdx.x * nw * cols + which * cols + 2 * rem) = s;
-  }
+  for (int e = threadIdx.x; e < nw * cols; e += 256)
+    partials[(long long)blockIdx.x * nw * cols + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
 }
 
 template <typename TD, typename TO>
-static bool ln_bwd_fast(int V2, int nblk, hipStream_t s, const TD* dy, long long lddy, const float* x, long long ldx,
-                        const float* mean, const float* rstd, const float* gamma, const float* g_in, float* g_out,
-                        TO* g_out_t, uint32_t seed, uint32_t thr, float dscale, float* partials, int rows,
-                        int want_col) {
-#define LNB(N) case N: hipLaunchKernelGGL((ln_bwd_vec<TD, TO, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows, want_col); return true;
-  switch (V2) { LNB(1) LNB(2) LNB(3) LNB(4) LNB(6) LNB(8) default: return false; }
+static bool ln_bwd_fast(int W, int cols, int nblk, hipStream_t s, const TD* dy, long long lddy, const float* x,
+                        long long ldx, const float* mean, const float* rstd, const float* gamma, const float* g_in,
+                        float* g_out, TO* g_out_t, uint32_t seed, uint32_t thr, float dscale, float* partials,
+                        int rows, int want_col) {
+#define LNB(WW, N) case N: hipLaunchKernelGGL((ln_bwd_vec<TD, TO, WW, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows, want_col); return true;
+  if (W == 4) {
+    switch (cols / 256) { LNB(4, 1) LNB(4, 2) LNB(4, 3) LNB(4, 4) default: return false; }
+  }
+  if (W == 2) {
+    switch (cols / 128) { LNB(2, 1) LNB(2, 2) LNB(2, 3) LNB(2, 4) LNB(2, 6) LNB(2, 8) default: return false; }
+  }
+  return false;
 #undef LNB
 }
 
-// sum the per-block partial rows: 64 columns per block, 4 row-interleaved accumulators
+// sum the per-block partial rows: 16 columns x 64 row lanes per block, 4 independent chains per
+// lane (16 loads in flight at nblk = 1024), fixed summation order
 // (nw = 2: dgamma|dbeta, nw = 3: dgamma|dbeta|dcol)
 __global__ __launch_bounds__(1024) void ln_param_reduce2(const float* __restrict__ partials, int nblk, int cols,
                                                          int nw, float* __restrict__ dgamma,
                                                          float* __restrict__ dbeta, float* __restrict__ dcol,
                                                          int accumulate) {
-  __shared__ float red[16][65];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + tx;
+  __shared__ float red[64][17];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + tx;
+  const long long ld = (long long)nw * cols;
   float s = 0.f;
   if (c < nw * cols) {
-#pragma unroll 4
-    for (int b = ty; b < nblk; b += 16) s += partials[(long long)b * nw * cols + c];
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = ty;
+    for (; b + 192 < nblk; b += 256)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += partials[(long long)(b + 64 * u) * ld + c];
+    for (; b < nblk; b += 64) s4[0] += partials[(long long)b * ld + c];
+    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   }
   red[ty][tx] = s;
   __syncthreads();
-  if (ty == 0 && c < nw * cols) {
-    float v = 0.f;
+  float v = 0.f;
+  if (ty < 8) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v += red[i][tx];
+    for (int i = 0; i < 8; ++i) v += red[ty * 8 + i][tx];
+  }
+  __syncthreads();
+  if (ty < 8) red[ty][tx] = v;
+  __syncthreads();
+  if (ty == 0 && c < nw * cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][tx];
     float* dst = c < cols ? dgamma + c : c < 2 * cols ? dbeta + (c - cols) : dcol + (c - 2 * cols);
-    *dst = accumulate ? *dst + v : v;
+    *dst = accumulate ? *dst + t : t;
   }
 }
 
@@ -367,26 +451,28 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
   const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   const float dscale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
   bool fast = false;
-  if (cols % 128 == 0 && cols <= 1024 && (lddy % 2) == 0 && (ldx % 2) == 0) {
-    const int V2 = cols / 128;
+  // W = 4 also needs 16-B aligned g_in / g_out rows (stride cols) and 8-B aligned branch rows
+  int W = ln_width(cols, x, ldx, dy, lddy, dy_dtype == CG_BF16 ? 2 : 4);
+  if (W == 4 && (((uintptr_t)g_out | (uintptr_t)g_in | (uintptr_t)g_out_t) & 15)) W = 2;
+  if (W) {
     if (dy_dtype == CG_BF16) {
       fast = out_dtype == CG_BF16
-                 ? ln_bwd_fast<bf16_t, bf16_t>(V2, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                 ? ln_bwd_fast<bf16_t, bf16_t>(W, cols, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
                                                g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col)
-                 : ln_bwd_fast<bf16_t, float>(V2, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                 : ln_bwd_fast<bf16_t, float>(W, cols, nblk, s, (const bf16_t*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
                                               g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col);
     } else {
       fast = out_dtype == CG_BF16
-                 ? ln_bwd_fast<float, bf16_t>(V2, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                 ? ln_bwd_fast<float, bf16_t>(W, cols, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
                                               g_out, (bf16_t*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col)
-                 : ln_bwd_fast<float, float>(V2, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
+                 : ln_bwd_fast<float, float>(W, cols, nblk, s, (const float*)dy, lddy, x, ldx, mean, rstd, gamma, g_in,
                                              g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col);
     }
   }
   if (fast) {
     CG_LAUNCH_CHECK();
     if (dgamma && dbeta) {
-      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 64)), dim3(1024), 0, s, partials, nblk,
+      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 16)), dim3(1024), 0, s, partials, nblk,
                          cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
       CG_LAUNCH_CHECK();
     }
