@@ -142,7 +142,7 @@ struct Acts {
   int32_t* seg;
   float* x;  // (L+1) x M x d
   std::vector<LayerAct> la;
-  float *meanf, *rstdf, *logits_int;
+  float *meanf, *rstdf, *logits_int, *logits_pad;
   void* xf;
   // backward scratch
   void *dlogits, *gT, *dbig, *dsmall;
@@ -187,6 +187,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.rstdf = w.take<float>(M * 4);
   A.xf = w.take<char>(M * d * es);
   A.logits_int = w.take<float>(M * D.V * 4);
+  A.logits_pad = w.take<float>(M * D.Vp * 4);  // head product at N = Vp (vector-epilogue tiles)
   const int noff = std::min(c->n_offsets, 8);
   A.oa.assign(noff, nullptr); A.og.assign(noff, nullptr); A.opj.assign(noff, nullptr);
   for (int i = 0; i < noff; ++i) {
@@ -344,6 +345,9 @@ int pick_split(const Ctx& C, int Mo, int N, long long K) {
   // 8 slabs suffice once there are >= 32 tiles; the 16-tile products (d x d at d512: attention
   // proj) run 218 -> 291 TF/s with 16 (dw_sweep on the box)
   if (s > (tiles > 16 ? 8 : MAX_SPLIT)) s = tiles > 16 ? 8 : MAX_SPLIT;
+  // > 32 tiles with long slabs: the most slabs that still fit one round at 2 blocks per CU
+  // (qkv at d512, 48 tiles, K = 16384: 10 slabs 51.6 us vs 8 slabs 55.5 us, dw_sweep on the box)
+  if (tiles > 32 && 512 / tiles > s && K / (512 / tiles) >= 1536) s = std::min<long long>(512 / tiles, MAX_SPLIT);
   if (s < 1) s = 1;
   if ((size_t)s * Mo * N > C.A.splitws_floats) s = 1;
   return (int)s;
@@ -543,11 +547,14 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   float* xL = A.x + (size_t)D.L * M * d;
   CK(cg_layernorm_fwd(C.dt, xL, d, P(C, C.Lo.lnfw), P(C, C.Lo.lnfb), A.xf, d, A.meanf, A.rstdf, (int)M, d, eps, C.s));
   const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
-  cg_gemm_desc g = lin_fwd(C, A.xf, d, hoff, d, D.V, d, m->logits, D.V);
+  // the head product runs at N = Vp (zero weight rows V..Vp-1) so that it takes the vector
+  // epilogue tiles; the loss reads the padded logits and the caller's (M, V) copy is compacted
+  cg_gemm_desc g = lin_fwd(C, A.xf, d, hoff, d, D.Vp, d, A.logits_pad, D.Vp);
   g.c_dtype = CG_F32;
   CK(cg_gemm(&g, C.s));
+  CK(cg_cast_pad_2d(A.logits_pad, D.Vp, (int)M, D.V, CG_F32, m->logits, D.V, D.V, C.s));
   if (targets) {
-    CK(cg_cross_entropy(m->logits, D.V, targets, (int)M, D.V, m->cfg.label_smoothing, m->loss_weights, 0, 1.0f, C.dt,
+    CK(cg_cross_entropy(A.logits_pad, D.Vp, targets, (int)M, D.V, m->cfg.label_smoothing, m->loss_weights, 0, 1.0f, C.dt,
                         A.dlogits, D.Vp, loss, A.cews, C.s));
   }
   return CG_OK;
