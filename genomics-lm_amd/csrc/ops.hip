@@ -514,13 +514,50 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   }
 }
 
+// d % 4 == 0: one wave per token row, 16-B column runs (no per-element index division)
+__global__ __launch_bounds__(256) void embed_fwd_rows_kernel(const int64_t* __restrict__ idx, const float* __restrict__ tok,
+                                                             const float* __restrict__ pos, float* __restrict__ x,
+                                                             int rows, int T, int d, uint32_t seed, uint32_t thr,
+                                                             float dscale) {
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= rows) return;
+  const int t = m % T;
+  const float4* tr = (const float4*)(tok + idx[m] * (long long)d);
+  const float4* pr = pos ? (const float4*)(pos + (long long)t * d) : nullptr;
+  float4* xr = (float4*)(x + (long long)m * d);
+  for (int q = lane; q < d / 4; q += 64) {
+    float4 v = tr[q];
+    if (pr) {
+      const float4 p = pr[q];
+      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    }
+    if (thr) {
+      const uint32_t c = 4u * (uint32_t)q;
+      v.x = cg_keep(seed, (uint32_t)m, c, thr) ? v.x * dscale : 0.f;
+      v.y = cg_keep(seed, (uint32_t)m, c + 1, thr) ? v.y * dscale : 0.f;
+      v.z = cg_keep(seed, (uint32_t)m, c + 2, thr) ? v.z * dscale : 0.f;
+      v.w = cg_keep(seed, (uint32_t)m, c + 3, thr) ? v.w * dscale : 0.f;
+    }
+    xr[q] = v;
+  }
+}
+
 extern "C" int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const float* pos_emb, float* x, int B,
                             int T, int d, uint32_t drop_seed, float drop_p, void* stream) {
   const long long total = (long long)B * T * d;
   if (total == 0) return CG_OK;
+  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
+  if (d % 4 == 0 && ((uintptr_t)tok_emb & 15) == 0 && ((uintptr_t)x & 15) == 0 &&
+      (!pos_emb || ((uintptr_t)pos_emb & 15) == 0)) {
+    const int rows = B * T;
+    hipLaunchKernelGGL(embed_fwd_rows_kernel, dim3(cg_cdiv(rows, 4)), dim3(256), 0, (hipStream_t)stream, idx, tok_emb,
+                       pos_emb, x, rows, T, d, drop_seed, thr, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
+    CG_LAUNCH_CHECK();
+    return CG_OK;
+  }
   int blocks = (int)((total + 255) / 256);
   if (blocks > 8192) blocks = 8192;
-  const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, idx, tok_emb, pos_emb, x,
                      B, T, d, drop_seed, thr, drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f);
   CG_LAUNCH_CHECK();
@@ -547,7 +584,22 @@ __global__ __launch_bounds__(256) void embed_bwd_tok_kernel(const int64_t* __res
   const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
   float* mine = acc + wave * V * 64;
   if (c < d) {
-    for (int r = r0 + wave; r < r1; r += 4) {
+    int r = r0 + wave;
+    for (; r + 28 < r1; r += 32) {  // 8 rows' loads in flight, added in row order
+      int tk[8];
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        tk[u] = (int)idx[r + 4 * u];
+        v[u] = g[(long long)(r + 4 * u) * d + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (thr) v[u] = cg_keep(seed, (uint32_t)(r + 4 * u), (uint32_t)c, thr) ? v[u] * dscale : 0.f;
+        mine[tk[u] * 64 + lane] += v[u];
+      }
+    }
+    for (; r < r1; r += 4) {
       const int tkn = (int)idx[r];
       float v = g[(long long)r * d + c];
       if (thr) v = cg_keep(seed, (uint32_t)r, (uint32_t)c, thr) ? v * dscale : 0.f;
@@ -569,6 +621,7 @@ __global__ void embed_bwd_tok_reduce(const float* __restrict__ part, float* __re
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= V * d) return;
   float s = 0.f;
+#pragma unroll 8
   for (int ch = 0; ch < nch; ++ch) s += part[(long long)ch * V * d + e];
   dtok[e] = accumulate ? dtok[e] + s : s;
 }
@@ -905,16 +958,24 @@ extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int 
 // Cross-entropy: label smoothing + class weights + ignore_index (F.cross_entropy,
 // model_tiny_gpt.py:343-349). L = sum_valid[(1-e) w_y nll_y + e/V sum_c w_c nll_c] / sum_valid w_y
 // ===========================================================================
-constexpr int CE_BLK = 256;   // rows per block = 4 waves x 1 row, grid-strided
+constexpr int CE_BLK = 4096;  // rows per block = 4 waves x 1 row, grid-strided beyond 16384 rows
+// sum_valid w_y: 1024 threads, 4 independent load chains each, fixed-order tree
 __global__ __launch_bounds__(1024) void ce_denom_kernel(const int64_t* __restrict__ tg, int rows, const float* __restrict__ w,
                                                         int ignore, float* __restrict__ ws) {
   __shared__ float red[1024];
-  float s = 0.f;
-  for (int r = threadIdx.x; r < rows; r += 1024) {
+  float s4[4] = {0.f, 0.f, 0.f, 0.f};
+  int r = threadIdx.x;
+  for (; r + 3072 < rows; r += 4096)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t t = tg[r + 1024 * u];
+      if (t != ignore) s4[u] += w ? w[t] : 1.0f;
+    }
+  for (; r < rows; r += 1024) {
     const int64_t t = tg[r];
-    if (t != ignore) s += w ? w[t] : 1.0f;
+    if (t != ignore) s4[0] += w ? w[t] : 1.0f;
   }
-  red[threadIdx.x] = s;
+  red[threadIdx.x] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
   __syncthreads();
   for (int o = 512; o > 0; o >>= 1) {
     if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
@@ -981,12 +1042,18 @@ __global__ __launch_bounds__(256) void ce_main_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) ws[1 + blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
 }
 
-__global__ void ce_final_kernel(const float* __restrict__ ws, int nblk, float* __restrict__ loss) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += ws[1 + b];
-    *loss = s / ws[0];
+// loss = sum of the per-block partials (fixed-order tree) / denominator
+__global__ __launch_bounds__(1024) void ce_final_kernel(const float* __restrict__ ws, int nblk, float* __restrict__ loss) {
+  __shared__ float red[1024];
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 1024) s += ws[1 + b];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 512; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) *loss = red[0] / ws[0];
 }
 
 static int ce_blocks(int rows) {
@@ -1011,7 +1078,7 @@ extern "C" int cg_cross_entropy(const float* logits, long long ldl, const int64_
                        class_w, ignore_index, grad_scale, (float*)dlogits, ldd, (float*)ws);
   CG_LAUNCH_CHECK();
   if (loss) {
-    hipLaunchKernelGGL(ce_final_kernel, dim3(1), dim3(64), 0, s, (const float*)ws, nblk, loss);
+    hipLaunchKernelGGL(ce_final_kernel, dim3(1), dim3(1024), 0, s, (const float*)ws, nblk, loss);
     CG_LAUNCH_CHECK();
   }
   return CG_OK;
