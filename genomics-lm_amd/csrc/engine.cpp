@@ -146,6 +146,8 @@ struct Acts {
   void* xf;
   // backward scratch
   void *dlogits, *gT, *dbig, *dsmall;
+  void* head2;  // bf16 mode: the head weight stacked twice [E; E] (2Vp x d), K operand of the split-dlogits dX
+  long long ldl;  // dlogits row stride: Vp, or 2 Vp for split bf16 (hi | lo)
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
   size_t splitws_floats;
   bool wT;  // transposed weight copies present
@@ -195,7 +197,9 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
     A.og[i] = w.take<char>(M * d * es);
     A.opj[i] = w.take<char>(M * d * es);
   }
-  A.dlogits = w.take<char>(M * D.Vp * es);
+  A.ldl = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
+  A.dlogits = w.take<char>(M * A.ldl * es);
+  A.head2 = c->dtype == CG_BF16 ? w.take<char>((size_t)2 * D.Vp * d * 2) : nullptr;
   A.gT = w.take<char>(M * d * es);
   const long long big = std::max<long long>({(long long)D.hid, 2LL * D.Hp, (long long)D.Nqkv});
   A.dbig = w.take<char>(M * big * es);
@@ -305,6 +309,27 @@ cg_gemm_desc lin_dx(const Ctx& C, const void* dy, long long lddy, long long woff
   }
   g.C = dx; g.ldc = lddx;
   return g;
+}
+// d[M,d] (fp32, + resid epilogue set by the caller) = dl[M,Vp] . E[Vp,d] for a head weight E:
+// in bf16 mode dl holds split-bf16 rows (hi | lo, CG_BF16X2) and the product runs over
+// K = 2 Vp against [E; E] (A.head2, filled by fill_head2)
+cg_gemm_desc head_dx(const Ctx& C, long long hoff, void* out, long long ldo) {
+  const Dims& D = C.D;
+  if (C.dt != CG_BF16) return lin_dx(C, C.A.dlogits, D.Vp, hoff, D.d, D.Vp, D.d, out, ldo);
+  cg_gemm_desc g = gdesc(C);
+  g.M = (int)C.M; g.N = D.d; g.K = 2 * D.Vp;
+  g.A = C.A.dlogits; g.lda = C.A.ldl; g.a_kcontig = 1;
+  g.B = C.A.head2; g.ldb = D.d; g.b_kcontig = 0;
+  g.C = out; g.ldc = ldo;
+  return g;
+}
+int fill_head2(const Ctx& C, long long hoff) {
+  if (C.dt != CG_BF16) return CG_OK;
+  const size_t bytes = (size_t)C.D.Vp * C.D.d * 2;
+  for (int i = 0; i < 2; ++i)
+    if (hipMemcpyAsync((char*)C.A.head2 + i * bytes, W(C, hoff), bytes, hipMemcpyDeviceToDevice, C.s) != hipSuccess)
+      return CG_ELAUNCH;
+  return CG_OK;
 }
 // refresh the transposed weight copies of every block (one batched launch per 64 matrices)
 int transpose_weights(const Ctx& C) {
@@ -427,12 +452,12 @@ int aux_backward(const Ctx& C, int accumulate) {
       continue;
     }
     if (!m->aux_ready) return CG_EINVAL;
-    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt, A.dlogits, D.Vp, D.Vp, C.s));
-    // d(head) += Gc^T . pj   (phase 0's own head product initialised it)
+    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, D.Vp, C.s));
+    // d(head) += Gc^T . pj   (phase 0's own head product initialised it; hi half of split rows)
     cg_gemm_desc g = gdesc(C);
     g.c_dtype = CG_F32;
     g.M = D.Vp; g.N = d; g.K = (int)M;
-    g.A = A.dlogits; g.lda = D.Vp; g.a_kcontig = 0;
+    g.A = A.dlogits; g.lda = A.ldl; g.a_kcontig = 0;
     g.B = A.opj[i]; g.ldb = d; g.b_kcontig = 0;
     g.C = G(C, hoff); g.ldc = d;
     g.epilogue = CG_EPI_ACCUM;
@@ -440,7 +465,8 @@ int aux_backward(const Ctx& C, int accumulate) {
     g.workspace = A.splitws;
     CK(cg_gemm(&g, C.s));
     // dpj = Gc . E ; the second Linear's grads
-    g = lin_dx(C, A.dlogits, D.Vp, hoff, d, D.Vp, d, A.dsmall, d);
+    g = head_dx(C, hoff, A.dsmall, d);
+    g.c_dtype = C.dt;
     CK(cg_gemm(&g, C.s));
     CK(lin_dw(C, A.dsmall, d, A.og[i], d, d, d, C.Lo.off2w[i], d, accumulate));
     CK(bias_grad(C, A.dsmall, d, d, C.Lo.off2b[i], accumulate));
@@ -554,8 +580,8 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   CK(cg_gemm(&g, C.s));
   CK(cg_cast_pad_2d(A.logits_pad, D.Vp, (int)M, D.V, CG_F32, m->logits, D.V, D.V, C.s));
   if (targets) {
-    CK(cg_cross_entropy(A.logits_pad, D.Vp, targets, (int)M, D.V, m->cfg.label_smoothing, m->loss_weights, 0, 1.0f, C.dt,
-                        A.dlogits, D.Vp, loss, A.cews, C.s));
+    CK(cg_cross_entropy(A.logits_pad, D.Vp, targets, (int)M, D.V, m->cfg.label_smoothing, m->loss_weights, 0, 1.0f,
+                        C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, loss, A.cews, C.s));
   }
   return CG_OK;
 }
@@ -613,12 +639,14 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   if (phase == 0) {
     CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+    CK(fill_head2(C, hoff));
     if (m->targets) {
-      // d(head weight) = s dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero)
+      // d(head weight) = s dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero; the hi
+      // half of split-bf16 rows)
       cg_gemm_desc g = gdesc(C);
       g.c_dtype = CG_F32;
       g.M = D.Vp; g.N = d; g.K = (int)M;
-      g.A = A.dlogits; g.lda = D.Vp; g.a_kcontig = 0;
+      g.A = A.dlogits; g.lda = A.ldl; g.a_kcontig = 0;
       g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
       g.C = G(C, hoff); g.ldc = d;
       g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
@@ -627,7 +655,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       g.workspace = A.splitws;
       CK(cg_gemm(&g, C.s));
       // dxf = s dlogits . E
-      g = lin_dx(C, A.dlogits, D.Vp, hoff, d, D.Vp, d, A.dtmp, d);
+      g = head_dx(C, hoff, A.dtmp, d);
       g.c_dtype = CG_F32;
       g.alpha = m->head_grad_scale;
       CK(cg_gemm(&g, C.s));

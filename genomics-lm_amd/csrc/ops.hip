@@ -984,7 +984,22 @@ __global__ __launch_bounds__(1024) void ce_denom_kernel(const int64_t* __restric
   if (threadIdx.x == 0) ws[0] = red[0];
 }
 
-template <typename TD>
+// SPLIT (dtype CG_BF16X2): g is stored as bf16 hi = bf16(g) at column c and bf16 lo =
+// bf16(g - hi) at column ldd/2 + c, so a bf16 MFMA product over [hi | lo] x [W; W] sees g to
+// ~16 significant bits (the tied-head dX product feeds ln_f's bias gradient, a column sum
+// over all tokens that cancels to a small value: 8-bit dlogits leave ~10% error in it).
+template <typename TD, bool SPLIT = false>
+__device__ __forceinline__ void st_grad(TD* dr, int c, long long half, float g) {
+  if constexpr (SPLIT) {
+    const bf16_t hi = f2bf(g);
+    dr[c] = hi;
+    dr[half + c] = f2bf(g - bf2f(hi));
+  } else {
+    st_act<TD>(dr + c, g);
+  }
+}
+
+template <typename TD, bool SPLIT = false>
 __global__ __launch_bounds__(256) void ce_main_kernel(const float* __restrict__ logits, long long ldl,
                                                       const int64_t* __restrict__ tg, int rows, int V, float eps,
                                                       const float* __restrict__ w, int ignore, float grad_scale,
@@ -1010,6 +1025,7 @@ __global__ __launch_bounds__(256) void ce_main_kernel(const float* __restrict__ 
     const float se = wave_sum(e0 + e1);
     const float lse = mx + __logf(se);
     TD* dr = dl ? dl + (long long)row * ldd : nullptr;
+    const long long half = SPLIT ? ldd / 2 : ldd;
     if (valid) {
       const float wy = w ? w[t] : 1.0f;
       // smoothing term sum_c w_c (lse - z_c)
@@ -1027,15 +1043,15 @@ __global__ __launch_bounds__(256) void ce_main_kernel(const float* __restrict__ 
             const float p = (k == 0 ? e0 : e1) * rse;
             const float wc = w ? w[c] : 1.f;
             float g = (1.0f - eps) * wy * (p - (c == t ? 1.f : 0.f)) + (eps / (float)V) * (Wt * p - wc);
-            st_act<TD>(dr + c, g * inv);
+            st_grad<TD, SPLIT>(dr, c, half, g * inv);
           }
         }
       }
     } else if (dr) {
-      for (int c = lane; c < V; c += 64) st_act<TD>(dr + c, 0.f);
+      for (int c = lane; c < V; c += 64) st_grad<TD, SPLIT>(dr, c, half, 0.f);
     }
     if (dr)
-      for (int c = V + lane; c < ldd; c += 64) st_act<TD>(dr + c, 0.f);
+      for (int c = V + lane; c < half; c += 64) st_grad<TD, SPLIT>(dr, c, half, 0.f);
   }
   if (lane == 0) wsum[wave] = acc;
   __syncthreads();
@@ -1070,9 +1086,13 @@ extern "C" int cg_cross_entropy(const float* logits, long long ldl, const int64_
   const int nblk = ce_blocks(rows);
   hipLaunchKernelGGL(ce_denom_kernel, dim3(1), dim3(1024), 0, s, targets, rows, class_w, ignore_index, (float*)ws);
   CG_LAUNCH_CHECK();
+  if (d_dtype == CG_BF16X2 && (ldd & 1 || ldd / 2 < V)) return CG_EINVAL;
   if (d_dtype == CG_BF16)
     hipLaunchKernelGGL(ce_main_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, logits, ldl, targets, rows, V, eps,
                        class_w, ignore_index, grad_scale, (bf16_t*)dlogits, ldd, (float*)ws);
+  else if (d_dtype == CG_BF16X2)
+    hipLaunchKernelGGL((ce_main_kernel<bf16_t, true>), dim3(nblk), dim3(256), 0, s, logits, ldl, targets, rows, V,
+                       eps, class_w, ignore_index, grad_scale, (bf16_t*)dlogits, ldd, (float*)ws);
   else
     hipLaunchKernelGGL(ce_main_kernel<float>, dim3(nblk), dim3(256), 0, s, logits, ldl, targets, rows, V, eps,
                        class_w, ignore_index, grad_scale, (float*)dlogits, ldd, (float*)ws);
@@ -1177,19 +1197,20 @@ extern "C" int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n,
 
 // fp32 [rows][cols] -> dtype [rows][dcols] with zero pad columns (aux-head logit grads into
 // the padded GEMM operand layout)
-template <typename T_>
+template <typename T_, bool SPLIT = false>
 __global__ __launch_bounds__(256) void cast_pad_kernel(const float* __restrict__ src, long long lds, int rows, int cols,
                                                        T_* __restrict__ dst, long long ldd, int dcols) {
   const long long total = (long long)rows * dcols;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const long long r = i / dcols;
     const int c = (int)(i - r * dcols);
-    st_act<T_>(dst + r * ldd + c, c < cols ? src[r * lds + c] : 0.f);
+    st_grad<T_, SPLIT>(dst + r * ldd, c, dcols, c < cols ? src[r * lds + c] : 0.f);
   }
 }
 extern "C" int cg_cast_pad_2d(const float* src, long long lds, int rows, int cols, int dtype, void* dst, long long ldd,
                               int dcols, void* stream) {
-  if (rows < 0 || cols < 0 || dcols < cols || lds < cols || ldd < dcols) return CG_EINVAL;
+  if (rows < 0 || cols < 0 || dcols < cols || lds < cols || ldd < (dtype == CG_BF16X2 ? 2 * dcols : dcols))
+    return CG_EINVAL;
   const long long total = (long long)rows * dcols;
   if (total == 0) return CG_OK;
   if (!src || !dst) return CG_EINVAL;
@@ -1198,6 +1219,9 @@ extern "C" int cg_cast_pad_2d(const float* src, long long lds, int rows, int col
   if (dtype == CG_BF16)
     hipLaunchKernelGGL(cast_pad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, lds, rows, cols,
                        (bf16_t*)dst, ldd, dcols);
+  else if (dtype == CG_BF16X2)
+    hipLaunchKernelGGL((cast_pad_kernel<bf16_t, true>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, lds, rows,
+                       cols, (bf16_t*)dst, ldd, dcols);
   else if (dtype == CG_F32)
     hipLaunchKernelGGL(cast_pad_kernel<float>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, src, lds, rows, cols,
                        (float*)dst, ldd, dcols);

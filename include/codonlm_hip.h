@@ -9,7 +9,9 @@
  * return CG_OK (0) or a negative cg_status.  Buffers are caller-owned device memory.
  *
  * dtype codes: CG_F32 = fp32 storage/compute (parity mode), CG_BF16 = bf16 storage
- * with fp32 accumulation (throughput mode).
+ * with fp32 accumulation (throughput mode), CG_BF16X2 = split bf16 (a value v stored as
+ * hi = bf16(v) and lo = bf16(v - hi) in the two halves of a row: [hi(ldd/2) | lo(ldd/2)]),
+ * accepted where noted (gradient operands whose later sums cancel).
  */
 #ifndef CODONLM_HIP_H
 #define CODONLM_HIP_H
@@ -20,7 +22,7 @@
 extern "C" {
 #endif
 
-enum { CG_F32 = 0, CG_BF16 = 1 };
+enum { CG_F32 = 0, CG_BF16 = 1, CG_BF16X2 = 2 };
 enum { CG_OK = 0, CG_EINVAL = -1, CG_EUNSUPPORTED = -2, CG_ELAUNCH = -3 };
 
 /* GEMM epilogue flags (bit set) */
@@ -125,8 +127,9 @@ int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
 
 /* Label-smoothed, class-weighted, ignore_index cross-entropy fwd+bwd over logits rows
  * (F.cross_entropy at model_tiny_gpt.py:343-349).  logits fp32 [rows][ldl], V used
- * columns; writes loss (1 float, mean per the reference weighting), dlogits (dtype,
- * pad columns [V,ldd) zeroed) scaled by `grad_scale`.  ws: cg_ce_workspace(rows) */
+ * columns; writes loss (1 float, mean per the reference weighting), dlogits (d_dtype
+ * CG_F32 / CG_BF16 / CG_BF16X2, pad columns [V, ldd) -- per half for CG_BF16X2 -- zeroed)
+ * scaled by `grad_scale`.  ws: cg_ce_workspace(rows) */
 size_t cg_ce_workspace(int rows);
 int cg_cross_entropy(const float* logits, long long ldl, const int64_t* targets, int rows,
                      int V, float eps, const float* class_w, int ignore_index,
@@ -166,7 +169,8 @@ int cg_transpose16_batch(const cg_transpose_batch* tb, void* stream);
 /* elementwise casts / utilities */
 int cg_cast_f32_to_bf16(const float* src, uint16_t* dst, long long n, void* stream);
 int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stream);
-/* dst[r][c] = src[r][c] (c < cols), 0 for cols <= c < dcols; dst in `dtype` */
+/* dst[r][c] = src[r][c] (c < cols), 0 for cols <= c < dcols; dst in `dtype` (CG_BF16X2: hi in
+ * columns [0, dcols), lo in [dcols, 2 dcols); ldd >= 2 dcols) */
 int cg_cast_pad_2d(const float* src, long long lds, int rows, int cols, int dtype, void* dst,
                    long long ldd, int dcols, void* stream);
 

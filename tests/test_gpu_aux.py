@@ -185,3 +185,36 @@ def test_scaled_loss_and_aux_only_backward():
         s = max(1e-3, float(r.abs().max()))
         err = float((p.grad.detach().cpu() - r).abs().max())
         assert err <= 2e-4 * s, (k, err, s)
+
+
+def test_adamw_fast_group_matches_oracle():
+    """The reference's two AdamW groups (loop.py:685-718): offset_projs / termination_head in the
+    fast group (lr_embedding, weight_decay 0), everything else -- embeddings, LN, biases -- in the
+    backbone group (lr, weight_decay).  FusedAdamW runs both as ranges of the flat buffer (the
+    fast params form its tail); two steps against the oracle's per-tensor AdamW fed the same
+    gradients."""
+    from codonlm_amd.optim import FusedAdamW
+    cfgd, g = load_golden("aux_objective")
+    gg = dict(g, param_seed=np.array(0))
+    m, cfg, params = make_model(cfgd, gg)
+    m.train()
+    x, y = _idx(g)
+    args = aux_objective_args(g)
+    lr, lr_emb, wd = 2e-3, 7e-3, 0.05
+    opt = FusedAdamW(m, lr=lr, weight_decay=wd, lr_embedding=lr_emb)
+    fast_names = {k for k, _ in m.named_parameters() if k.startswith(("offset_projs", "termination_head"))}
+    assert fast_names and len(opt.param_groups) == 2
+    P = {k: p.detach().cpu().clone() for k, p in m.named_parameters()}
+    mo = {k: torch.zeros_like(v) for k, v in P.items()}
+    vo = {k: torch.zeros_like(v) for k, v in P.items()}
+    for step in (1, 2):
+        opt.zero_grad()
+        _objective(m, x, y, cfg, args).backward()
+        grads = {k: p.grad.detach().cpu().clone() for k, p in m.named_parameters()}
+        opt.step()
+        for k in P:
+            fast = k in fast_names
+            O.adamw_step(P[k], grads[k], mo[k], vo[k], step, lr_emb if fast else lr, 0.0 if fast else wd)
+    for k, p in m.named_parameters():
+        atol = 2.5 * lr if k.endswith("attn.key.bias") else 2e-6
+        np.testing.assert_allclose(p.detach().cpu().numpy(), P[k].numpy(), rtol=1e-5, atol=atol, err_msg=k)

@@ -1,0 +1,190 @@
+"""The BASELINE geometries on both engines vs the pinned oracle.
+
+The bf16 engine is the path behind every throughput number (persistent / LDS-DMA MFMA
+GEMMs, the dW tiles, the 32x32x16 MFMA attention kernels), so it is pinned here at the
+real kernel shapes -- d512 hd64 T1024, d384 hd48 KV4 T512 with RoPE + SwiGLU, d256 T512,
+d384 hd48 with the five offset heads + termination head -- against the CPU oracle
+(oracle/tinygpt_oracle.py, itself pinned to the reference's golden vectors).  Each config
+runs 2 layers at B=2 (C1 keeps its 4 layers) so the oracle's fp32 autograd finishes in
+seconds; every kernel sees the full-size T, d, hd and head layout of the config.
+
+Bounds.  fp32 engine: the north-star 1e-4 (logits relative to the logit scale, loss, and
+every parameter gradient relative to its largest entry).  bf16 engine: bf16 storage of
+weights and activations (8 significant bits, rounding 2^-9 relative per value) with fp32
+accumulation everywhere; through 2-4 residual blocks, the head and the loss that gives
+relative L2 errors of a few 1e-3 (measured 1.0-1.9e-3 logits, <= 9.1e-3 grads), so the bounds are
+rel-L2 <= 5e-3 for logits and
+<= 1.5e-2 for every parameter gradient (without RoPE the key biases are exactly zero in exact
+arithmetic -- softmax shift invariance -- and are only checked to be at noise level).
+ln_f.bias's gradient is the column sum over all tokens of d(loss)/d(xf) = dlogits . E, which
+cancels to a small value; the engine therefore keeps dlogits as split bf16 (hi + lo,
+CG_BF16X2) for that product, and it is held to the same bound as every other gradient.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import tinygpt_oracle as O
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+LOGIT_REL_L2_BF16 = 5e-3
+GRAD_REL_L2_BF16 = 1.5e-2
+TOL_FP32 = 1e-4
+
+# (oracle config kwargs, microbatch B); C5 = stage2.6_large_scaling + its aux heads
+CONFIGS = {
+    "C1": (dict(n_layer=4, n_head=2, n_embd=128, block_size=512), 2),
+    "C2": (dict(n_layer=2, n_head=4, n_embd=256, block_size=512), 2),
+    "C3": (dict(n_layer=2, n_head=8, n_kv_head=4, n_embd=384, block_size=512, use_swiglu=True, use_rope=True,
+                loss_weights=None), 2),
+    "C4": (dict(n_layer=2, n_head=8, n_embd=512, block_size=1024), 2),
+    "C5": (dict(n_layer=2, n_head=8, n_embd=384, block_size=512, termination_aux=True,
+                multi_offset_targets=[2, 4, 8, 16, 32]), 2),
+}
+OFFSET_W = {2: 0.2, 4: 0.2, 8: 0.2, 16: 0.2, 32: 0.2}
+TERM_W = 0.1
+
+
+def _eos_weights(V=68, w=3.0):
+    lw = [1.0] * V
+    for t in (2, 52, 54, 60):  # <EOS_CDS>, TAA, TAG, TGA (loop.py:396-405)
+        lw[t] = w
+    return lw
+
+
+def packed_batch(B, T, seed):
+    """Packed CDS windows: BOS .. codons .. EOS, SEP between CDSs, a PAD tail on the last row."""
+    rng = np.random.default_rng(seed)
+    tok = rng.integers(4, 68, size=(B, T + 1))
+    for b in range(B):
+        p = 0
+        while p < T + 1:
+            n = int(rng.integers(40, 400))
+            tok[b, p] = 1
+            e = min(T, p + n)
+            tok[b, e] = 2
+            if e + 1 <= T:
+                tok[b, e + 1] = 3
+            p = e + 2
+    tok[-1, -(T // 7):] = 0
+    return tok[:, :-1].copy(), tok[:, 1:].copy()
+
+
+def _cfg(name, label_smoothing=0.05):
+    kw, B = CONFIGS[name]
+    kw = dict(kw)
+    if name == "C3":
+        kw["loss_weights"] = _eos_weights()
+    return O.OracleConfig(vocab_size=68, label_smoothing=label_smoothing, **kw), B
+
+
+def _model(cfg, params, dtype):
+    from codonlm_amd import TinyGPT
+    m = TinyGPT(cfg.vocab_size, cfg.block_size, n_layer=cfg.n_layer, n_head=cfg.n_head, n_embd=cfg.n_embd,
+                dropout=0.0, label_smoothing=cfg.label_smoothing, sep_id=cfg.sep_id, n_kv_head=cfg.n_kv_head,
+                loss_weights=cfg.loss_weights, termination_aux=cfg.termination_aux,
+                multi_offset_targets=cfg.multi_offset_targets or None, use_swiglu=cfg.use_swiglu,
+                use_rope=cfg.use_rope, compute_dtype=dtype, device=DEV)
+    missing, unexpected = m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
+    assert not unexpected
+    m.train()
+    return m
+
+
+def _gpu_objective(m, cfg, x, y):
+    from codonlm_amd.training import objectives as obj
+    if not (cfg.termination_aux or cfg.multi_offset_targets):
+        logits, loss = m(x, y)
+        return logits, loss, loss
+    logits, loss, aux = m(x, y, return_aux=True)
+    off_total, _ = obj.multi_offset_lm_loss(aux["offset_logits"], y, OFFSET_W, label_smoothing=cfg.label_smoothing)
+    labels = obj.termination_distance_bucket_labels(y, stop_ids=(2,))
+    term = obj.termination_aux_loss(aux["termination_logits"], labels)
+    return logits, loss, loss + off_total + TERM_W * term
+
+
+def _oracle(cfg, params, x, y):
+    if not (cfg.termination_aux or cfg.multi_offset_targets):
+        o, grads = O.forward_backward(cfg, params, x, y)
+        return o["logits"].detach(), float(o["loss"]), float(o["loss"]), grads
+    parts, grads = O.objective_backward(cfg, params, x, y, OFFSET_W, TERM_W, (2,))
+    with torch.no_grad():
+        o = O.forward(cfg, params, x, y)
+    return o["logits"], float(parts["loss"]), float(parts["total"]), grads
+
+
+def _rel_l2(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / max(1e-30, float(b.norm())))
+
+
+_REF_CACHE = {}
+
+
+def _reference(name):
+    if name not in _REF_CACHE:
+        cfg, B = _cfg(name)
+        params = O.synthetic_params(cfg, seed=11 + len(name))
+        x, y = packed_batch(B, cfg.block_size, seed=5)
+        torch.set_num_threads(max(1, min(16, torch.get_num_threads())))
+        _REF_CACHE[name] = (cfg, params, x, y, _oracle(cfg, params, x, y))
+    return _REF_CACHE[name]
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_bf16_engine_matches_oracle(name):
+    cfg, params, x, y, (rlogits, rloss, rtotal, rgrads) = _reference(name)
+    m = _model(cfg, params, "bf16")
+    xd, yd = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    logits, loss, total = _gpu_objective(m, cfg, xd, yd)
+    total.backward()
+    torch.cuda.synchronize()
+    lg = logits.detach().float().cpu()
+    el = _rel_l2(lg, rlogits)
+    assert el <= LOGIT_REL_L2_BF16, (name, "logits", el)
+    assert abs(loss.item() - rloss) <= 1e-2 * abs(rloss), (name, loss.item(), rloss)
+    assert abs(total.item() - rtotal) <= 1e-2 * abs(rtotal), (name, total.item(), rtotal)
+    # greedy next-codon ids agree wherever the oracle's top-2 margin exceeds the bf16 logit error
+    top2 = torch.topk(rlogits, 2, dim=-1).values
+    margin = (top2[..., 0] - top2[..., 1])
+    resolvable = margin > 4 * LOGIT_REL_L2_BF16 * float(rlogits.abs().max())
+    agree = (lg.argmax(-1) == rlogits.argmax(-1)) | ~resolvable
+    assert bool(agree.all()), (name, int((~agree).sum()))
+    worst, noise = [], []
+    for k, p in m.named_parameters():
+        ref = rgrads[k]
+        got = p.grad.detach().float().cpu()
+        if k.endswith("attn.key.bias") and not cfg.use_rope:  # (RoPE breaks the shift invariance)
+            scale = max(float(rgrads[k.replace("key.bias", "query.bias")].abs().max()), 1e-6)
+            noise.append((float(got.abs().max()) / scale, k))
+            continue
+        worst.append((_rel_l2(got, ref), k))
+    worst.sort(reverse=True)
+    print(f"[{name} bf16] logits rel-L2 {el:.2e}; worst grads {[(k, f'{e:.2e}') for e, k in worst[:4]]}")
+    assert worst[0][0] <= GRAD_REL_L2_BF16, (name, worst[:4])
+    assert all(r <= 2e-2 for r, _ in noise), (name, noise)
+
+
+@pytest.mark.parametrize("name", sorted(CONFIGS))
+def test_fp32_engine_matches_oracle(name):
+    cfg, params, x, y, (rlogits, rloss, rtotal, rgrads) = _reference(name)
+    m = _model(cfg, params, "fp32")
+    xd, yd = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    logits, loss, total = _gpu_objective(m, cfg, xd, yd)
+    total.backward()
+    lg = logits.detach().cpu()
+    scale = max(1.0, float(rlogits.abs().max()))
+    assert float((lg - rlogits).abs().max()) <= TOL_FP32 * scale, name
+    assert abs(loss.item() - rloss) <= TOL_FP32 * max(1.0, abs(rloss)), name
+    assert abs(total.item() - rtotal) <= TOL_FP32 * max(1.0, abs(rtotal)), name
+    # bit-exact greedy ids wherever the oracle's top-2 margin is resolvable at fp32
+    top2 = torch.topk(rlogits, 2, dim=-1).values
+    resolvable = (top2[..., 0] - top2[..., 1]) > 1e-3 * scale
+    assert bool(((lg.argmax(-1) == rlogits.argmax(-1)) | ~resolvable).all()), name
+    for k, p in m.named_parameters():
+        ref = rgrads[k]
+        s = max(1e-3, float(ref.abs().max()))
+        err = float((p.grad.detach().cpu() - ref).abs().max())
+        assert err <= 2 * TOL_FP32 * s, (name, k, err, s)

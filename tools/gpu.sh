@@ -1,0 +1,50 @@
+# One entry point for GPU-box work (run as: gpurun -- 'bash tools/gpu.sh <cmd> [args]').
+# Every GPU step has its own time limit and the steps chain with && (a failure ends the call).
+#
+#   test  [pytest -k expr]      GPU tests (tests -m gpu), one process      -> gpurun_out/test/
+#   full                        round-end gate: all GPU tests, then smoke() -> gpurun_out/full/
+#   bench [bench.py args]       one bench line                               -> gpurun_out/bench/
+#   prof  [tag] [bench args]    rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/prof_<tag>/
+#   pmc   <tag> <script> "<counter set>" ["<counter set>" ...]
+#                               one rocprofv3 --pmc pass per counter set over python <script>
+#                                                                            -> gpurun_out/pmc_<tag>/
+set -u
+cmd=${1:-test}
+shift || true
+export TMPDIR=/tmp
+PYT="python -u -m pytest -p no:cacheprovider --timeout 300 --timeout-method thread"
+case "$cmd" in
+  test)
+    mkdir -p gpurun_out/test
+    if [ $# -gt 0 ]; then k=(-k "$1"); else k=(); fi
+    timeout -k 10 900 $PYT tests -m gpu -x -q "${k[@]}" > gpurun_out/test/pytest.log 2>&1
+    rc=$?; tail -5 gpurun_out/test/pytest.log; exit $rc ;;
+  full)
+    mkdir -p gpurun_out/full
+    timeout -k 10 900 $PYT tests -m gpu -x -q > gpurun_out/full/pytest.log 2>&1 &&
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/full/smoke.log 2>&1
+    rc=$?; tail -3 gpurun_out/full/pytest.log; exit $rc ;;
+  bench)
+    mkdir -p gpurun_out/bench
+    timeout -k 10 600 python bench.py "$@" > gpurun_out/bench/bench.json 2> gpurun_out/bench/bench.err
+    rc=$?; cat gpurun_out/bench/bench.json; exit $rc ;;
+  prof)
+    tag=${1:-step}; shift || true
+    O=gpurun_out/prof_$tag
+    mkdir -p $O
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- \
+      python bench.py --no-cpu-baseline --no-kernel-roofline "$@" > $O/bench.log 2>&1
+    rc=$?; tail -2 $O/bench.log; exit $rc ;;
+  pmc)
+    tag=$1; script=$2; shift 2
+    O=gpurun_out/pmc_$tag
+    mkdir -p $O
+    i=0
+    for ctrs in "$@"; do
+      i=$((i+1))
+      timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctrs -d $O/p$i -o run --output-format csv -- \
+        python $script > $O/p$i.log 2>&1 || exit 1
+    done ;;
+  *)
+    echo "unknown command $cmd"; exit 2 ;;
+esac
