@@ -16,7 +16,7 @@ import torch  # noqa: F401  -- must precede the CDLL load (shared HIP runtime)
 # CG_LIB_PATH: load another build of the same library (same-box A/B of two builds)
 LIB_PATH = Path(os.environ.get("CG_LIB_PATH") or Path(__file__).resolve().parent / "libcodonlm_hip.so")
 
-CG_F32, CG_BF16 = 0, 1
+CG_F32, CG_BF16, CG_BF16X2 = 0, 1, 2
 CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1, 2, 4, 8, 16, 32, 64
 PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV = range(7)
@@ -41,6 +41,18 @@ class GemmDesc(C.Structure):
                 ("bias", vp), ("resid", vp), ("ldr", i64),
                 ("aux", vp), ("aux_out", vp), ("ld_aux", i64),
                 ("drop_seed", u32), ("drop_p", f32), ("split_k", i32), ("workspace", vp)]
+
+
+DW_MAX = 16
+
+
+class DwProduct(C.Structure):
+    _fields_ = [("A", vp), ("lda", i64), ("B", vp), ("ldb", i64), ("C", vp), ("ldc", i64),
+                ("N_out", i32), ("K_out", i32), ("alpha", f32), ("accumulate", i32)]
+
+
+class DwGroup(C.Structure):
+    _fields_ = [("n", i32), ("K", i32), ("tile_m", i32), ("p", DwProduct * DW_MAX)]
 
 
 class AdamwSegment(C.Structure):
@@ -77,7 +89,7 @@ class Model(C.Structure):
                 ("B", i32), ("T", i32), ("training", i32), ("window", i32), ("seed", u32),
                 ("idx", vp), ("targets", vp), ("logits", vp),
                 ("aux_ready", i32), ("head_grad_scale", f32), ("d_term_logits", vp), ("ld_d_term", i64),
-                ("d_offset_logits", vp * 8)]
+                ("d_offset_logits", vp * 8), ("dw_done_layer", i32)]
 
 
 # name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
@@ -85,6 +97,9 @@ SIGNATURES = {
     "cg_gemm": (i32, [C.POINTER(GemmDesc), vp]),
     "cg_gemm_set_wide": (i32, [i32]),
     "cg_gemm_set_pers": (i32, [i32]),
+    "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),
+    "cg_gemm_dw_tiles": (i32, [i32, i32, i32]),
+    "cg_gemm_dw_set_tile": (i32, [i32]),
     "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
     "cg_layernorm_bwd_blocks": (i32, [i32]),
     "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, vp, vp,

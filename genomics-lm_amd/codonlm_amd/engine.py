@@ -236,14 +236,19 @@ class Engine:
                 f"cg_model_backward(phase={phase}, layer={layer})")
 
     def backward(self, accumulate: bool = False, bucket_hook=None):
-        """Full backward; ``bucket_hook(name)`` runs after each phase (DDP overlap point)."""
+        """Full backward; ``bucket_hook(name)`` runs as soon as a bucket's gradients are final
+        (the DDP overlap point): "head" after phase 0, block l once its dW group has been
+        issued (cg_model.dw_done_layer), "embed" after phase 2."""
         self.backward_phase(0, 0, accumulate)
         if bucket_hook:
             bucket_hook("head")
+        done = self.cfg.n_layer
         for layer in range(self.cfg.n_layer - 1, -1, -1):
             self.backward_phase(1, layer, accumulate)
             if bucket_hook:
-                bucket_hook(layer)
+                for b in range(done - 1, self.model.dw_done_layer - 1, -1):
+                    bucket_hook(b)
+            done = min(done, self.model.dw_done_layer)
         self.backward_phase(2, 0, accumulate)
         if bucket_hook:
             bucket_hook("embed")

@@ -264,3 +264,34 @@ def transpose16(mats):
     if mats:
         L.check(L.lib.cg_transpose16_batch(C.byref(tb), L.stream_ptr(mats[0].device)), "cg_transpose16_batch")
     return outs
+
+
+def gemm_dw_grouped(products, *, tile_m=0):
+    """Grouped weight gradients: for each (dy [K, N_out] bf16, x [K, K_out] bf16, out fp32
+    [N_out, K_out], alpha, accumulate) -> out (+)= alpha * dy^T x, one persistent launch
+    (cg_gemm_dw_grouped).  Row strides are taken from the tensors."""
+    if not products:
+        return
+    if len(products) > L.DW_MAX:
+        raise ValueError(f"at most {L.DW_MAX} products per group")
+    g = L.DwGroup()
+    g.n, g.tile_m = len(products), int(tile_m)
+    K = None
+    for i, (dy, x, out, alpha, acc) in enumerate(products):
+        for t in (dy, x, out):
+            L.require_device(t, "gemm_dw_grouped")
+        if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32:
+            raise ValueError("gemm_dw_grouped: bf16 operands, fp32 output")
+        if K is None:
+            K = dy.shape[0]
+        if dy.shape[0] != K or x.shape[0] != K:
+            raise ValueError("gemm_dw_grouped: every product reduces over the same K rows")
+        p = g.p[i]
+        p.A, p.lda, p.B, p.ldb = dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0)
+        p.C, p.ldc = out.data_ptr(), out.stride(0)
+        p.N_out, p.K_out = dy.shape[1], x.shape[1]
+        if tuple(out.shape) != (p.N_out, p.K_out):
+            raise ValueError("gemm_dw_grouped: out must be [N_out, K_out]")
+        p.alpha, p.accumulate = float(alpha), int(bool(acc))
+    g.K = int(K)
+    L.check(L.lib.cg_gemm_dw_grouped(C.byref(g), L.stream_ptr(products[0][0].device)), "cg_gemm_dw_grouped")

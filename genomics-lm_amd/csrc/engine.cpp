@@ -25,6 +25,7 @@ enum { SITE_EMB = 0, SITE_ATTN = 1, SITE_MLP = 2 };
 
 struct Dims {
   int V, Vp, Tmax, L, H, KV, d, hd, kvd, Nqkv, hid, Hp, swiglu, rope;
+  int G;  // blocks per grouped weight-gradient launch (dw_plan)
 };
 
 bool dims_of(const cg_model_cfg* c, Dims& D) {
@@ -43,7 +44,42 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   D.rope = c->use_rope != 0;
   D.hid = D.swiglu ? (int)(8 * (long long)c->n_embd / 3) : 4 * c->n_embd;
   D.Hp = D.swiglu ? (int)rup(D.hid, 64) : D.hid;
+  D.G = 1;
   return true;
+}
+
+int device_cus() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    n = v;
+  }
+  return n;
+}
+// Blocks per grouped dW launch (bf16 engine).  A group's tiles run as one persistent launch with
+// one workgroup per CU and every tile costing about the same (full-token reduction), so the
+// launch takes ceil(tiles / CUs) rounds: pick the group size with the fewest rounds per block,
+// the smaller group on ties (its gradients are final -- and all-reduced -- earlier).
+// CG_DW_GROUP forces a size.
+int dw_plan(const cg_model_cfg* c, const Dims& D) {
+  if (c->dtype != CG_BF16 || D.L <= 0) return 1;
+  static const int forced = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
+  const int gmax = std::min(D.L, CG_DW_MAX / 4);
+  if (forced > 0) return std::min(forced, gmax);
+  const int d = D.d;
+  const int per_layer = cg_gemm_dw_tiles(0, D.Nqkv, d) + cg_gemm_dw_tiles(0, d, d) +
+                        (D.swiglu ? cg_gemm_dw_tiles(0, 2 * D.Hp, d) + cg_gemm_dw_tiles(0, d, D.Hp)
+                                  : cg_gemm_dw_tiles(0, D.hid, d) + cg_gemm_dw_tiles(0, d, D.hid));
+  const int cus = device_cus();
+  int best = 1;
+  double best_cost = 1e30;
+  for (int g = 1; g <= gmax; ++g) {
+    const double cost = (double)((g * per_layer + cus - 1) / cus) / g;
+    if (cost < best_cost - 1e-9) best_cost = cost, best = g;
+  }
+  return best;
 }
 
 struct Layout {
@@ -138,14 +174,21 @@ struct LayerAct {
   // bf16 mode: per-step transposed copies of the shadow weights (K-contiguous dX operands)
   void *qkvT, *pT, *w1T, *w2T, *wguT, *wdT;
 };
+// per-block gradient operands kept until the block's grouped dW launch (slot = position of
+// the block inside its group): dY of fc2/down (gin), of fc1/gate|up (dmlp), of proj (gattn),
+// of qkv (dqkv), all in the compute dtype
+struct DwSlot {
+  void *gin, *gattn, *dmlp, *dqkv;
+};
 struct Acts {
   int32_t* seg;
+  std::vector<DwSlot> slot;
   float* x;  // (L+1) x M x d
   std::vector<LayerAct> la;
   float *meanf, *rstdf, *logits_int, *logits_pad;
   void* xf;
   // backward scratch
-  void *dlogits, *gT, *dbig, *dsmall;
+  void *dlogits, *dbig, *dsmall;
   void* head2;  // bf16 mode: the head weight stacked twice [E; E] (2Vp x d), K operand of the split-dlogits dX
   long long ldl;  // dlogits row stride: Vp, or 2 Vp for split bf16 (hi | lo)
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
@@ -199,8 +242,14 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   }
   A.ldl = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
   A.dlogits = w.take<char>(M * A.ldl * es);
+  A.slot.resize(D.G);
+  for (auto& sl : A.slot) {
+    sl.gin = w.take<char>(M * d * es);
+    sl.gattn = w.take<char>(M * d * es);
+    sl.dmlp = w.take<char>(M * (D.swiglu ? 2LL * D.Hp : (long long)D.hid) * es);
+    sl.dqkv = w.take<char>(M * D.Nqkv * es);
+  }
   A.head2 = c->dtype == CG_BF16 ? w.take<char>((size_t)2 * D.Vp * d * 2) : nullptr;
-  A.gT = w.take<char>(M * d * es);
   const long long big = std::max<long long>({(long long)D.hid, 2LL * D.Hp, (long long)D.Nqkv});
   A.dbig = w.take<char>(M * big * es);
   A.dsmall = w.take<char>(M * std::max(d, D.Hp) * es);
@@ -250,6 +299,7 @@ struct Ctx {
 
 int make_ctx(const cg_model* m, int B, int T, void* stream, Ctx& C) {
   if (!dims_of(&m->cfg, C.D)) return CG_EINVAL;
+  C.D.G = dw_plan(&m->cfg, C.D);
   build_layout(&m->cfg, C.D, C.Lo);
   C.m = m;
   C.B = B; C.T = T; C.M = (long long)B * T;
@@ -397,6 +447,46 @@ int bias_grad(const Ctx& C, const void* dy, long long lddy, int N, long long gof
 
 float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 
+// position of block l inside its dW group (groups run from block L-1 downwards)
+int slot_of(const Dims& D, int l) { return (D.L - 1 - l) % D.G; }
+bool group_ends(const Dims& D, int l) { return l == 0 || slot_of(D, l) == D.G - 1; }
+
+// The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
+// bf16 mode (gemm_dw.h), the per-product GEMMs in fp32 parity mode.
+int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
+  const Dims& D = C.D;
+  const int d = D.d;
+  cg_dw_group grp;
+  memset(&grp, 0, sizeof(grp));
+  grp.K = (int)C.M;
+  auto add = [&](const void* dy, int n_out, const void* x, int k_out, long long goff) -> int {
+    if (C.dt != CG_BF16) return lin_dw(C, dy, n_out, x, k_out, n_out, k_out, goff, k_out, accumulate);
+    cg_dw_product& q = grp.p[grp.n++];
+    q.A = dy; q.lda = n_out;
+    q.B = x; q.ldb = k_out;
+    q.C = G(C, goff); q.ldc = k_out;
+    q.N_out = n_out; q.K_out = k_out;
+    q.alpha = 1.0f; q.accumulate = accumulate;
+    return CG_OK;
+  };
+  for (int l = l_hi; l >= l_lo; --l) {
+    const auto& o = C.Lo.lay[l];
+    const auto& a = C.A.la[l];
+    const DwSlot& sl = C.A.slot[slot_of(D, l)];
+    if (!D.swiglu) {
+      CK(add(sl.gin, d, a.g, D.hid, o.w2));
+      CK(add(sl.dmlp, D.hid, a.h2, d, o.w1));
+    } else {
+      CK(add(sl.gin, d, a.s, D.Hp, o.wd));
+      CK(add(sl.dmlp, 2 * D.Hp, a.h2, d, o.wgu));
+    }
+    CK(add(sl.gattn, d, a.y, d, o.wp));
+    CK(add(sl.dqkv, D.Nqkv, a.h1, d, o.wqkv));
+  }
+  if (C.dt == CG_BF16 && grp.n) return cg_gemm_dw_grouped(&grp, C.s);
+  return CG_OK;
+}
+
 int zero_grad(const Ctx& C, long long off, long long elems) {
   return hipMemsetAsync(G(C, off), 0, (size_t)elems * 4, C.s) == hipSuccess ? CG_OK : CG_ELAUNCH;
 }
@@ -503,6 +593,7 @@ extern "C" int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* ou
 extern "C" size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T) {
   Dims D;
   if (!dims_of(cfg, D)) return 0;
+  D.G = dw_plan(cfg, D);
   Acts A;
   return carve(cfg, D, B, T, nullptr, A);
 }
@@ -670,8 +761,9 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     const int ll = D.L - 1;
     // gT feeds block L-1's MLP output Linear: its bias gradient (GELU mode) is gT's column sum
     float* db2 = (D.L > 0 && !D.swiglu) ? G(C, C.Lo.lay[ll].b2) : nullptr;
+    m->dw_done_layer = D.L;
     CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xL, d, A.meanf, A.rstdf, P(C, C.Lo.lnfw), nullptr, A.g, C.dt,
-                        D.L > 0 ? A.gT : nullptr, site_seed(seed, ll, SITE_MLP), D.L > 0 ? p : 0.f, A.lnpart,
+                        D.L > 0 ? A.slot[slot_of(D, ll)].gin : nullptr, site_seed(seed, ll, SITE_MLP), D.L > 0 ? p : 0.f, A.lnpart,
                         G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), db2, accumulate, (int)M, d, eps, C.s));
     return CG_OK;
   }
@@ -681,49 +773,50 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     const auto& o = C.Lo.lay[l];
     const auto& a = A.la[l];
     float* xl = A.x + (size_t)l * M * d;
-    // ---------------- MLP branch: gT = dL/d(mlp out) (dropout mask applied)
+    const DwSlot& sl = A.slot[slot_of(D, l)];
+    // ---------------- MLP branch: sl.gin = dL/d(mlp out) (dropout mask applied); the weight
+    // gradients of the block are produced by its group's flush_dw from the slot operands
     if (!D.swiglu) {
-      // (b2's gradient was produced by the LayerNorm backward that wrote gT)
-      CK(lin_dw(C, A.gT, d, a.g, D.hid, d, D.hid, o.w2, D.hid, accumulate));
+      // (b2's gradient was produced by the LayerNorm backward that wrote gin)
       // dGELU product; its fused column sums (64-row partials) are fc1's bias gradient
-      cg_gemm_desc g = lin_dx(C, A.gT, d, o.w2, D.hid, d, D.hid, A.dbig, D.hid, a.w2T);
+      cg_gemm_desc g = lin_dx(C, sl.gin, d, o.w2, D.hid, d, D.hid, sl.dmlp, D.hid, a.w2T);
       g.epilogue = CG_EPI_DGELU | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
       g.workspace = A.splitws;
       CK(cg_gemm(&g, C.s));
       CK(cg_colsum_reduce(A.splitws, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
-      CK(lin_dw(C, A.dbig, D.hid, a.h2, d, D.hid, d, o.w1, d, accumulate));
-      g = lin_dx(C, A.dbig, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
+      g = lin_dx(C, sl.dmlp, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
       CK(cg_gemm(&g, C.s));
     } else {
-      CK(lin_dw(C, A.gT, d, a.s, D.Hp, d, D.Hp, o.wd, D.Hp, accumulate));
-      cg_gemm_desc g = lin_dx(C, A.gT, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp, a.wdT);
+      cg_gemm_desc g = lin_dx(C, sl.gin, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp, a.wdT);
       CK(cg_gemm(&g, C.s));
-      CK(cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, A.dbig, 2 * D.Hp, (int)M, D.hid, C.s));
-      CK(lin_dw(C, A.dbig, 2 * D.Hp, a.h2, d, 2 * D.Hp, d, o.wgu, d, accumulate));
-      g = lin_dx(C, A.dbig, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dsmall, d, a.wguT);
+      CK(cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, sl.dmlp, 2 * D.Hp, (int)M, D.hid, C.s));
+      g = lin_dx(C, sl.dmlp, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dsmall, d, a.wguT);
       CK(cg_gemm(&g, C.s));
     }
-    // gT = dL/d(proj out); its column sum is the proj bias gradient
-    CK(cg_layernorm_bwd(C.dt, A.dsmall, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, A.gT, 0, 0.f,
+    // gattn = dL/d(proj out); its column sum is the proj bias gradient
+    CK(cg_layernorm_bwd(C.dt, A.dsmall, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, sl.gattn, 0, 0.f,
                         A.lnpart, G(C, o.ln2w), G(C, o.ln2b), G(C, o.bp), accumulate, (int)M, d, eps, C.s));
     // ---------------- attention branch
-    CK(lin_dw(C, A.gT, d, a.y, d, d, d, o.wp, d, accumulate));
-    cg_gemm_desc g = lin_dx(C, A.gT, d, o.wp, d, d, d, A.dsmall, d, a.pT);
+    cg_gemm_desc g = lin_dx(C, sl.gattn, d, o.wp, d, d, d, A.dsmall, d, a.pT);
     CK(cg_gemm(&g, C.s));
-    CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, A.dbig,
+    CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, sl.dqkv,
                    D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, A.delta, C.s));
     if (D.rope)
-      CK(cg_rope_tab(C.dt, A.dbig, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
-    CK(lin_dw(C, A.dbig, D.Nqkv, a.h1, d, D.Nqkv, d, o.wqkv, d, accumulate));
-    CK(bias_grad(C, A.dbig, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
-    g = lin_dx(C, A.dbig, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
+      CK(cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
+    CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
+    g = lin_dx(C, sl.dqkv, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
     CK(cg_gemm(&g, C.s));
-    // gT feeds block l-1's MLP output Linear (bias grad fused as above; lands in block l-1's
-    // gradient range, which is all-reduced only after phase l-1)
+    // the group's weight gradients once its lowest block is done
+    if (group_ends(D, l)) {
+      CK(flush_dw(C, l + slot_of(D, l), l, accumulate));
+      m->dw_done_layer = l;
+    }
+    // block l-1's MLP output gradient (its bias grad fused as above; it lands in block l-1's
+    // gradient range, which is final only after block l-1's group)
     float* db2 = (l > 0 && !D.swiglu) ? G(C, C.Lo.lay[l - 1].b2) : nullptr;
     CK(cg_layernorm_bwd(C.dt, A.dsmall, d, xl, d, a.mean1, a.rstd1, P(C, o.ln1w), A.g, A.g, C.dt,
-                        l > 0 ? A.gT : nullptr, site_seed(seed, l - 1, SITE_MLP), l > 0 ? p : 0.f, A.lnpart,
-                        G(C, o.ln1w), G(C, o.ln1b), db2, accumulate, (int)M, d, eps, C.s));
+                        l > 0 ? A.slot[slot_of(D, l - 1)].gin : nullptr, site_seed(seed, l - 1, SITE_MLP),
+                        l > 0 ? p : 0.f, A.lnpart, G(C, o.ln1w), G(C, o.ln1b), db2, accumulate, (int)M, d, eps, C.s));
     return CG_OK;
   }
   if (phase == 2) {

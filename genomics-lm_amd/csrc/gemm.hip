@@ -446,6 +446,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
 
 #include "gemm_wide.h"
 #include "gemm_pers.h"
+#include "gemm_dw.h"
 
 // CG_EPI_COLSUM fallback: part[r/64][n] = sum of C rows [64r, 64r+64) (column n)
 __global__ __launch_bounds__(256) void colsum64_kernel(const void* C, long long ldc, int ct, int M, int N,
@@ -687,4 +688,75 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     CG_LAUNCH_CHECK();
   }
   return CG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// grouped weight-gradient GEMM (gemm_dw.h)
+// ---------------------------------------------------------------------------
+static int g_dw_bm = [] {
+  const char* e = getenv("CG_DW_BM");
+  return e ? atoi(e) : 128;
+}();
+extern "C" int cg_gemm_dw_set_tile(int bm) {
+  const int old = g_dw_bm;
+  if (bm == 128 || bm == 129 || bm == 256) g_dw_bm = bm;
+  return old;
+}
+extern "C" int cg_gemm_dw_tiles(int bm, int N_out, int K_out) {
+  if (bm != 128 && bm != 129 && bm != 256) bm = g_dw_bm;
+  return cg_cdiv(N_out, bm == 256 ? 256 : 128) * cg_cdiv(K_out, bfd::BN);
+}
+template <int BM, int NS>
+static int launch_dw(bfd::Params& P, hipStream_t s) {
+  using G = bfd::Geo<BM, NS>;
+  int ntiles = 0;
+  for (int i = 0; i < P.nprod; ++i) {
+    bfd::Prod& pr = P.p[i];
+    pr.tiles_n = cg_cdiv(pr.K_out, bfd::BN);
+    pr.tile0 = ntiles;
+    ntiles += cg_cdiv(pr.N_out, BM) * pr.tiles_n;
+  }
+  P.ntiles = ntiles;
+  if (!ntiles) return CG_OK;
+  const int grid = std::min(ntiles, cu_count());
+  (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+  double flops = 0;
+  for (int i = 0; i < P.nprod; ++i) flops += 2.0 * P.p[i].N_out * (double)P.p[i].K_out * P.K;
+  cg_probe_begin(CG_PROBE_GEMM_DW, s);
+  hipLaunchKernelGGL((gemm_dw_kernel<BM, NS>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
+  cg_probe_end(CG_PROBE_GEMM_DW, s, flops);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
+  if (!grp || grp->n < 0 || grp->n > CG_DW_MAX || grp->K <= 0 || grp->K % bfd::BKT) return CG_EINVAL;
+  bfd::Params P{};
+  P.nprod = 0;
+  P.K = grp->K;
+  const long long lim = (1ll << 31) - (1ll << 24);
+  for (int i = 0; i < grp->n; ++i) {
+    const cg_dw_product& q = grp->p[i];
+    if (q.N_out <= 0 || q.K_out <= 0) continue;
+    if (!q.A || !q.B || !q.C) return CG_EINVAL;
+    if (q.N_out % 8 || q.K_out % 8 || q.lda % 8 || q.ldb % 8 || q.ldc % 4 || q.lda < q.N_out || q.ldb < q.K_out ||
+        q.ldc < q.K_out)
+      return CG_EUNSUPPORTED;
+    if (((uintptr_t)q.A & 15) || ((uintptr_t)q.B & 15) || ((uintptr_t)q.C & 15)) return CG_EUNSUPPORTED;
+    if (((long long)(grp->K - 1) * q.lda + q.N_out) * 2 >= lim || ((long long)(grp->K - 1) * q.ldb + q.K_out) * 2 >= lim)
+      return CG_EUNSUPPORTED;
+    bfd::Prod& pr = P.p[P.nprod++];
+    pr.A = (const bf16_t*)q.A; pr.lda = q.lda;
+    pr.B = (const bf16_t*)q.B; pr.ldb = q.ldb;
+    pr.C = q.C; pr.ldc = q.ldc;
+    pr.N_out = q.N_out; pr.K_out = q.K_out;
+    pr.alpha = q.alpha; pr.accum = q.accumulate;
+  }
+  if (!P.nprod) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int bm = grp->tile_m > 0 ? grp->tile_m : g_dw_bm;
+  // tile_m codes: 128 / 256 = rows of the C tile (ring of 4 / 3 stages); 129 / 257 = the same
+  // tile with one more ring stage (5 / 4... 160 KB LDS for 128)
+  if (bm == 256) return launch_dw<256, 3>(P, s);
+  if (bm == 129) return launch_dw<128, 5>(P, s);
+  return launch_dw<128, 4>(P, s);
 }

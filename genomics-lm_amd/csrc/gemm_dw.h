@@ -1,0 +1,222 @@
+// Grouped weight-gradient GEMM for the TinyGPT backward (included by gemm.hip).
+//
+//   dW_p[n][k] (+)= alpha_p * sum_m dY_p[m][n] X_p[m][k]      (every nn.Linear weight of a
+//   block: qkv, proj, fc1/fc2 or gate|up / down -- the autograd of model_tiny_gpt.py:85-93,
+//   132, 143-148, 50-57)
+//
+// Both operands are token-major ([M][cols], the reduction index m is the strided one), so the
+// tiles are DMA'd into LDS as [64 m-rows][128 cols] images (lane-linear LDS-DMA destination,
+// XOR swizzle applied on the per-lane source address) and the MFMA fragments are read with
+// ds_read_b64_tr_b16 (bfg::frag<false>).
+//
+// Every output tile is reduced over the WHOLE token range inside one workgroup: no split-K
+// slabs, no reduction pass -- the fp32 result is written once (HBM traffic = the operands
+// once + dW once).  The tiles of several products (one or more blocks' weights) form one
+// persistent launch so that there are enough of them to fill the CUs; each workgroup walks
+// its tiles with one LDS-DMA ring that runs across tile seams (stages are addressed by a
+// global step index; steps past the end DMA from an out-of-range offset, which the buffer
+// range check turns into zero fills, so every wave issues the same number of VMEM ops and
+// the counted vmcnt waits stay exact).
+//
+// The MFMA operands are swapped (D^T = X_frag x dY_frag), so each lane ends with 4
+// consecutive output columns of each 16x16 block: the epilogue is 16-byte stores straight
+// from the accumulators.
+namespace bfd {
+constexpr int BN = 128, BKT = 64;
+
+// LDS-DMA hidden from the compiler: with the builtin, hipcc cannot prove that the
+// ds_read_b64_tr_b16 fragment reads of the current stage do not alias the DMA writes into the
+// next slot and drains vmcnt(0) before every fragment read (the whole ring serialises).  The
+// kernel counts these DMAs itself (explicit vmcnt + barrier before a stage is read).  M0 (the
+// LDS destination base) is saved and restored around the load.
+__device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds), "s"(r)
+      : "memory");
+}
+
+template <int BM, int NSTAGE>
+struct Geo {
+  static constexpr int WAVES = BM / 32;                   // (BM/64) x 2 waves of 64x64
+  static constexpr int THREADS = WAVES * 64;
+  static constexpr int STAGES = NSTAGE;
+  static constexpr int A_BYTES = BM * BKT * 2;
+  static constexpr int B_BYTES = BN * BKT * 2;
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int A_CHUNKS = A_BYTES / 1024 / WAVES;  // 4
+  static constexpr int B_CHUNKS = B_BYTES / 1024 / WAVES;  // 4 (BM 128) or 2 (BM 256)
+  static constexpr int DPS = A_CHUNKS + B_CHUNKS;          // DMA wave-instructions per stage
+  static constexpr int SMEM = STAGES * STAGE_BYTES;
+};
+
+struct Prod {
+  const bf16_t* A;  // dY [K][lda], columns 0..N_out-1
+  const bf16_t* B;  // X  [K][ldb], columns 0..K_out-1
+  float* C;         // dW [N_out][ldc]
+  long long lda, ldb, ldc;
+  int N_out, K_out, tiles_n, tile0;
+  float alpha;
+  int accum;
+};
+struct Params {
+  Prod p[CG_DW_MAX];
+  int nprod, K, ntiles;
+};
+}  // namespace bfd
+
+template <int BM, int NSTAGE>
+__global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_kernel(const bfd::Params P) {
+  using namespace bfd;
+  using G = Geo<BM, NSTAGE>;
+  constexpr int S = G::STAGES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const int nblk = gridDim.x;
+  const int lb = cg_xcd_remap(blockIdx.x, nblk);  // an XCD's workgroups take consecutive tiles
+  const int my_tiles = lb < P.ntiles ? (P.ntiles - 1 - lb) / nblk + 1 : 0;
+  const int nt = P.K / BKT;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  if (my_tiles == 0) return;
+
+  auto find = [&](int tile, int& pi) {
+    pi = 0;
+    while (pi + 1 < P.nprod && tile >= P.p[pi + 1].tile0) ++pi;
+  };
+  // DMA cursor: the stage (local tile dk, k-step dt) the next issue() loads, with its
+  // product's buffer resources, tile origin and per-lane source offsets (rebuilt per tile)
+  uint32_t va[G::A_CHUNKS], vb[G::B_CHUNKS];
+  __amdgpu_buffer_rsrc_t ra, rb;
+  uint32_t a_org = 0, b_org = 0, a_step = 0, b_step = 0;
+  int dk = 0, dt = 0;
+  auto load_tile = [&]() {
+    if (dk >= my_tiles) {  // past the end: every DMA reads out of range (zero fill)
+      a_org = b_org = 0x80000000u;
+      a_step = b_step = 0;
+      return;
+    }
+    int pi;
+    const int tile = lb + dk * nblk;
+    find(tile, pi);
+    const Prod& pr = P.p[pi];
+    const int lt = tile - pr.tile0;
+    const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BN;
+    ra = __builtin_amdgcn_make_buffer_rsrc((void*)pr.A, (short)0,
+                                           (int)(((long long)(P.K - 1) * pr.lda + pr.N_out) * 2), 0x00020000);
+    rb = __builtin_amdgcn_make_buffer_rsrc((void*)pr.B, (short)0,
+                                           (int)(((long long)(P.K - 1) * pr.ldb + pr.K_out) * 2), 0x00020000);
+    a_org = (uint32_t)m0 * 2;
+    b_org = (uint32_t)n0 * 2;
+    a_step = (uint32_t)(BKT * pr.lda * 2);
+    b_step = (uint32_t)(BKT * pr.ldb * 2);
+#pragma unroll
+    for (int i = 0; i < G::A_CHUNKS; ++i) va[i] = bfw::src_off<false>((wave + G::WAVES * i) * 1024 + 16 * lane, pr.lda);
+#pragma unroll
+    for (int i = 0; i < G::B_CHUNKS; ++i) vb[i] = bfw::src_off<false>((wave + G::WAVES * i) * 1024 + 16 * lane, pr.ldb);
+  };
+  auto advance = [&]() {
+    if (++dt == nt) {
+      dt = 0;
+      ++dk;
+      load_tile();
+    }
+  };
+  auto issue = [&](int g) {
+    const uint32_t st = lds0 + (g % S) * G::STAGE_BYTES + wave * 1024;
+    const uint32_t ao = a_org + dt * a_step, bo = b_org + dt * b_step;
+#pragma unroll
+    for (int i = 0; i < G::A_CHUNKS; ++i) dma16_asm(ra, st + G::WAVES * i * 1024, ao + va[i]);
+#pragma unroll
+    for (int i = 0; i < G::B_CHUNKS; ++i) dma16_asm(rb, st + G::A_BYTES + G::WAVES * i * 1024, bo + vb[i]);
+    advance();
+  };
+
+  v4f acc[4][4];
+  auto step = [&](int g) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * G::DPS) : "memory");
+    __builtin_amdgcn_s_barrier();
+    const char* st = smem + (g % S) * G::STAGE_BYTES;
+    const char* as = st + (wm >> 7) * 16384;
+    const int ar = wm & 127;
+    const char* bs = st + G::A_BYTES;
+    v8bf af[2][4], bfr[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[0][i] = bfg::frag<false>(as, ar + 16 * i, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[0][j] = bfg::frag<false>(bs, wn + 16 * j, 0, lane);
+    // the DMAs of stage g + S - 1 go into the slot step g - 1 read (every wave is past it)
+    const uint32_t nx = lds0 + ((g + S - 1) % S) * G::STAGE_BYTES + wave * 1024;
+    const uint32_t ao = a_org + dt * a_step, bo = b_org + dt * b_step;
+#pragma unroll
+    for (int gr = 0; gr < 8; ++gr) {
+      const int i = gr >> 1, j0 = 2 * (gr & 1);
+      acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0], af[0][i], acc[i][j0], 0, 0, 0);
+      acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
+      if (gr < 4) af[1][gr] = bfg::frag<false>(as, ar + 16 * gr, 1, lane);
+      else bfr[1][gr - 4] = bfg::frag<false>(bs, wn + 16 * (gr - 4), 1, lane);
+      if (gr < G::A_CHUNKS) dma16_asm(ra, nx + G::WAVES * gr * 1024, ao + va[gr]);
+      else if (gr < G::DPS) dma16_asm(rb, nx + G::A_BYTES + G::WAVES * (gr - G::A_CHUNKS) * 1024, bo + vb[gr - G::A_CHUNKS]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // half 0's fragment reads (2 tr-reads each)
+#pragma unroll
+    for (int gr = 0; gr < 8; ++gr) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      if (gr < G::DPS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    advance();
+  };
+
+  auto epilogue = [&](int k) {
+    const int tile = lb + k * nblk;
+    int pi;
+    find(tile, pi);
+    const Prod& pr = P.p[pi];
+    const int lt = tile - pr.tile0;
+    const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BN;
+    const int g4 = lane >> 4, r16 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm + 16 * i + r16;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + wn + 16 * j + 4 * g4;
+        if (m < pr.N_out && n < pr.K_out) {
+          float4* c = (float4*)(pr.C + (long long)m * pr.ldc + n);
+          float4 v = make_float4(acc[i][j][0] * pr.alpha, acc[i][j][1] * pr.alpha, acc[i][j][2] * pr.alpha,
+                                 acc[i][j][3] * pr.alpha);
+          if (pr.accum) {
+            const float4 o = *c;
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *c = v;
+        }
+      }
+    }
+  };
+
+  load_tile();
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(s);
+  int g = 0;
+  for (int k = 0; k < my_tiles; ++k) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < nt; ++t, ++g) step(g);
+    epilogue(k);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
+}

@@ -71,6 +71,29 @@ int cg_gemm_set_wide(int mode);
  * Returns the previous mode. */
 int cg_gemm_set_pers(int mode);
 
+/* Grouped weight-gradient GEMM: for every product p of the group
+ *   C_p[n][k] (+)= alpha_p * sum_{m < K} A_p[m*lda_p + n] * B_p[m*ldb_p + k]
+ * (dW = dY^T X of the nn.Linear call sites, A = dY and B = X both token-major bf16, C fp32).
+ * Each output tile is reduced over all K rows inside one workgroup (no split-K partials);
+ * the tiles of all products form one persistent launch (tile_m = 128 or 256 rows of C per
+ * tile, 0 = default; env CG_DW_BM).  K % 64 == 0; N_out, K_out, lda, ldb % 8 == 0; ldc % 4. */
+#define CG_DW_MAX 16
+typedef struct {
+  const void* A; long long lda;
+  const void* B; long long ldb;
+  float* C; long long ldc;
+  int N_out, K_out;
+  float alpha; int accumulate;
+} cg_dw_product;
+typedef struct {
+  int n, K, tile_m;
+  cg_dw_product p[CG_DW_MAX];
+} cg_dw_group;
+int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream);
+/* tiles one product contributes at tile_m (0 = current default); default tile_m setter */
+int cg_gemm_dw_tiles(int tile_m, int N_out, int K_out);
+int cg_gemm_dw_set_tile(int tile_m);
+
 /* LayerNorm (nn.LayerNorm, biased var, eps) -- model_tiny_gpt.py:137,139,216 */
 int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,
                      const float* beta, void* y, long long ldy, float* mean, float* rstd,
@@ -276,6 +299,11 @@ typedef struct {
   const float* d_term_logits;       /* fp32 [B*T][ld_d_term] or NULL                    */
   long long ld_d_term;
   const float* d_offset_logits[8];  /* fp32 [B*T][V] per offset head, or NULL           */
+  /* set by cg_model_backward: the weight gradients of blocks are produced in groups (one
+   * grouped dW launch per group of blocks, bf16 engine); after each call every parameter
+   * gradient of blocks >= dw_done_layer (and of the head / ln_f after phase 0) is final --
+   * the point a data-parallel caller may start that bucket's all-reduce. */
+  int dw_done_layer;
 } cg_model;
 
 /* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
@@ -293,7 +321,8 @@ int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, in
 int cg_model_aux_forward(cg_model* m, float* term_logits, long long ld_term,
                          float* const* offset_logits, long long ld_off, void* stream);
 /* backward in phases so the caller can overlap per-bucket gradient all-reduce:
- *   phase 0: head (+ aux heads) + ln_f; phase 1: one block `layer` (call L-1 .. 0);
+ *   phase 0: head (+ aux heads) + ln_f; phase 1: one block `layer` (call L-1 .. 0; block
+ *   weight gradients complete per dW group, see cg_model.dw_done_layer);
  *   phase 2: embeddings.  Phase 0 scales the next-codon head gradient by head_grad_scale
  *   and adds the aux-head gradients given in d_term_logits / d_offset_logits; aux
  *   parameters without a gradient are zeroed when accumulate=0.
