@@ -88,7 +88,8 @@ class Model(C.Structure):
                 ("workspace", vp), ("workspace_bytes", sz),
                 ("B", i32), ("T", i32), ("training", i32), ("window", i32), ("seed", u32),
                 ("idx", vp), ("targets", vp), ("logits", vp),
-                ("aux_ready", i32), ("head_grad_scale", f32), ("d_term_logits", vp), ("ld_d_term", i64),
+                ("aux_ready", i32), ("head_grad_scale", f32), ("head_grad_scale_dev", vp), ("d_term_logits", vp),
+                ("ld_d_term", i64),
                 ("d_offset_logits", vp * 8), ("dw_done_layer", i32)]
 
 
@@ -124,6 +125,7 @@ SIGNATURES = {
     "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),
     "cg_cast_pad_2d": (i32, [vp, i64, i32, i32, i32, vp, i64, i32, vp]),
+    "cg_scale_dev": (i32, [i32, vp, i64, i32, i32, vp, vp]),
     "cg_gather_windows": (i32, [i32, vp, i64, i64, vp, i32, i32, vp, vp]),
     "cg_gather_sequences": (i32, [i32, vp, vp, vp, i64, vp, i32, i32, vp, vp, vp]),
     "cg_pool_hidden": (i32, [i32, vp, i64, vp, i32, i32, i32, i32, i32, C.POINTER(u32), vp, vp]),

@@ -181,13 +181,18 @@ class DeviceBatchLoader:
     """Iterates (x, y) device batches in the reference DataLoader's order.
 
     ``rank``/``world`` shard the batch sequence round-robin for data parallelism (rank r
-    takes batches r, r+world, ...), each rank keeping the same global order; with world > 1
-    every rank runs floor(n_batches / world) batches so per-group collectives stay matched."""
+    takes batches r, r+world, ...), each rank keeping the same global order.  Training
+    (``drop_remainder=True``): every rank runs floor(n_batches / world) batches so the
+    per-group collectives stay matched.  Evaluation (``drop_remainder=False``): the first
+    n_batches % world ranks run one batch more, so every batch is evaluated exactly once and
+    the sums reduced over ranks do not depend on the GPU count."""
 
     def __init__(self, ds: DeviceCodonDataset, batch_size: int, *, shuffle: bool = False, seed: int | None = None,
-                 bucket_batching: bool = False, n_buckets: int = 8, rank: int = 0, world: int = 1):
+                 bucket_batching: bool = False, n_buckets: int = 8, rank: int = 0, world: int = 1,
+                 drop_remainder: bool = True):
         self.ds, self.bs = ds, int(batch_size)
         self.rank, self.world = int(rank), max(1, int(world))
+        self.drop_remainder = bool(drop_remainder)
         n = len(ds)
         self.order, self._bounds = epoch_batches(n, self.bs, shuffle=shuffle, seed=seed,
                                                  lengths=ds.seq_lengths if (bucket_batching and ds.is_dynamic) else None,
@@ -195,17 +200,21 @@ class DeviceBatchLoader:
         self._order_dev = torch.from_numpy(self.order).to(ds.device) if n else None
 
     def __len__(self):
-        nb = len(self._bounds) - 1
-        if self.world > 1:
-            return nb // self.world
-        return nb
+        return len(self.shard())
 
     def global_batches(self) -> int:
         return len(self._bounds) - 1
 
+    def shard(self) -> list:
+        """Global batch indices this rank runs, in order."""
+        nb = len(self._bounds) - 1
+        if self.world == 1:
+            return list(range(nb))
+        n = nb // self.world if self.drop_remainder else (nb - self.rank + self.world - 1) // self.world
+        return [self.rank + j * self.world for j in range(max(0, n))]
+
     def __iter__(self):
-        for j in range(len(self)):
-            k = self.rank + j * self.world
+        for k in self.shard():
             a, b = int(self._bounds[k]), int(self._bounds[k + 1])
             yield self.ds.gather(self._order_dev[a:b], self.order[a:b])
 

@@ -205,12 +205,19 @@ class Engine:
                 "cg_model_aux_forward")
         return term, [o[:, :cfg.vocab_size] for o in offs]
 
-    def set_head_grads(self, scale: float, d_term=None, d_offsets=None):
-        """Gradients phase 0 consumes: the next-codon loss scale and the aux-head logit
-        gradients (fp32, flattened to (M, cols)); None = that head is unused."""
+    def set_head_grads(self, scale: float, d_term=None, d_offsets=None, scale_dev=None):
+        """Gradients phase 0 consumes: the next-codon loss scale (host float, times the device
+        float ``scale_dev`` when given -- the autograd output gradient, read in-kernel so the
+        backward needs no host sync) and the aux-head logit gradients (fp32, flattened to
+        (M, cols)); None = that head is unused."""
         m = self.model
         m.head_grad_scale = float(scale)
         keep = []
+        m.head_grad_scale_dev = None
+        if scale_dev is not None:
+            sd = scale_dev.detach().reshape(1).to(torch.float32).contiguous()
+            keep.append(sd)
+            m.head_grad_scale_dev = sd.data_ptr()
         m.d_term_logits, m.ld_d_term = None, 0
         if d_term is not None:
             t = d_term.reshape(-1, d_term.shape[-1]).to(torch.float32).contiguous()

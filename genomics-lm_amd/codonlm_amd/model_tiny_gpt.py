@@ -143,6 +143,17 @@ class Block(nn.Module):
                                      nn.Dropout(dropout))
 
 
+def mix_seed_rank(seed: int, rank: int) -> int:
+    """Dropout seed of a data-parallel rank: the shared step counter with the rank mixed in
+    (identity for rank 0)."""
+    if not rank:
+        return int(seed) & 0xFFFFFFFF
+    x = (int(seed) ^ (int(rank) * 0x85EBCA6B)) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    return x ^ (x >> 15)
+
+
 class _EngineBackward(torch.autograd.Function):
     """Autograd node tying ``loss`` to the native backward (loop.py:1233 loss.backward())."""
 
@@ -260,6 +271,11 @@ class TinyGPT(nn.Module):
         self._grads_fresh = True
         self._accum_next = False
         self._dropout_seed = 0
+        # data-parallel rank mixed into the dropout seeds (ranks draw independent masks for the
+        # same step; rank 0 keeps the single-process sequence) and the per-backward bucket hook
+        # a data-parallel caller sets before loss.backward() (engine.backward's overlap point)
+        self._seed_rank = 0
+        self._bucket_hook = None
 
     # ------------------------------------------------------------------ layout/views
     def _view(self, buf, spec):
@@ -384,13 +400,15 @@ class TinyGPT(nn.Module):
     def _native_backward(self, gout, d_term=None, d_offsets=None):
         """Native backward of the last forward: ``gout`` = d(objective)/d(loss) (None when the
         next-codon loss is unused), ``d_term`` / ``d_offsets`` = gradients of the aux logits."""
-        scale = 0.0 if gout is None else float(gout.detach().float().item())
         # an optimizer that set grads to None means "fresh group"
         if self.tok_emb.weight.grad is None:
             self._grads_fresh = True
         eng = self.engine
-        eng.set_head_grads(scale, d_term, d_offsets)
-        eng.backward(accumulate=not self._grads_fresh)
+        # d(objective)/d(loss) stays on the device: the engine scales the head gradient in-kernel
+        eng.set_head_grads(0.0 if gout is None else 1.0, d_term, d_offsets,
+                           scale_dev=None if gout is None else gout)
+        hook, self._bucket_hook = self._bucket_hook, None
+        eng.backward(accumulate=not self._grads_fresh, bucket_hook=hook)
         self._grads_fresh = False
         self._bind_grad_views()
 
@@ -427,7 +445,7 @@ class TinyGPT(nn.Module):
 
     def next_dropout_seed(self) -> int:
         self._dropout_seed = (self._dropout_seed + 0x9E3779B9) & 0xFFFFFFFF
-        return self._dropout_seed
+        return mix_seed_rank(self._dropout_seed, self._seed_rank)
 
     def forward(self, idx, targets=None, return_aux: bool = False, shape_embeddings=None,
                 attention_window: int | None = None):
@@ -495,4 +513,4 @@ def num_params(model: TinyGPT) -> int:
     return sum(p.numel() for p in model.parameters())
 
 
-__all__ = ["TinyGPT", "num_params"]
+__all__ = ["TinyGPT", "num_params", "mix_seed_rank"]

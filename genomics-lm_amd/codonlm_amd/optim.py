@@ -37,21 +37,14 @@ class FusedAdamW(torch.optim.Optimizer):
             groups.append({"params": [p for _, p in backbone], "lr": lr, "weight_decay": weight_decay})
         super().__init__(groups, dict(lr=lr, weight_decay=weight_decay, betas=betas, eps=eps))
         self.betas, self.eps = betas, eps
-        # every group must be one contiguous range of the flat buffer
+        # the groups run as contiguous ranges of the flat buffer: the fast params (aux heads) are
+        # laid out last by cg_model_param_layout, so they form its tail
         base = flat.data_ptr()
         total = flat.numel()
-        self._ranges = []
-        spans = []
-        for g in self.param_groups:
-            offs = [((p.data_ptr() - base) // 4) for p in g["params"]]
-            ends = [o + (p.storage_offset() - p.storage_offset()) for o, p in zip(offs, g["params"])]
-            del ends
-            spans.append(offs)
-        fast_begin = min(spans[0]) if fast else total
-        if fast:
-            self._ranges = [(fast_begin, total), (0, fast_begin)]
-        else:
-            self._ranges = [(0, total)]
+        fast_begin = min((p.data_ptr() - base) // 4 for _, p in fast) if fast else total
+        if any((p.data_ptr() - base) // 4 >= fast_begin for _, p in backbone):
+            raise RuntimeError("FusedAdamW: the fast parameter group is not the tail of the flat buffer")
+        self._ranges = [(fast_begin, total), (0, fast_begin)] if fast else [(0, total)]
         self.exp_avg = torch.zeros_like(flat)
         self.exp_avg_sq = torch.zeros_like(flat)
         self.step_count = 0
@@ -59,20 +52,52 @@ class FusedAdamW(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = True):
         self.model.zero_grad(set_to_none)
 
+    def _moment_view(self, buf, p):
+        off = (p.data_ptr() - self.model.flat_parameters().data_ptr()) // 4
+        return buf.as_strided(p.shape, p.stride(), buf.storage_offset() + off)
+
     def state_dict(self):
-        """torch's param_groups (lr/wd the schedulers drive) + the flat moments and step."""
+        """torch.optim.AdamW's format -- param_groups (the lr / wd the schedulers drive) and a
+        per-parameter 'state' {step, exp_avg, exp_avg_sq} whose moments are views of the flat
+        moment buffers -- plus 'flat_state' (the flat buffers themselves).  The reference trainer
+        (torch.optim.AdamW.load_state_dict) resumes from the per-parameter state; this
+        optimizer from either."""
+        self.state.clear()
+        if self.step_count > 0:
+            for g in self.param_groups:
+                for p in g["params"]:
+                    self.state[p] = {"step": torch.tensor(float(self.step_count)),
+                                     "exp_avg": self._moment_view(self.exp_avg, p),
+                                     "exp_avg_sq": self._moment_view(self.exp_avg_sq, p)}
         sd = super().state_dict()
+        self.state.clear()
         sd["flat_state"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": int(self.step_count)}
         return sd
 
     def load_state_dict(self, state_dict):
         flat = state_dict.get("flat_state")
-        super().load_state_dict({k: v for k, v in state_dict.items() if k != "flat_state"})
-        if flat is not None:
-            with torch.no_grad():
+        per_param = state_dict.get("state") or {}
+        super().load_state_dict({"state": {}, "param_groups": state_dict["param_groups"]})
+        with torch.no_grad():
+            if flat is not None:
                 self.exp_avg.copy_(flat["exp_avg"])
                 self.exp_avg_sq.copy_(flat["exp_avg_sq"])
-            self.step_count = int(flat["step"])
+                self.step_count = int(flat["step"])
+            elif per_param:
+                # a torch.optim.AdamW state (the reference trainer's checkpoints): moments per
+                # parameter index, in param_groups order
+                params = [p for g in self.param_groups for p in g["params"]]
+                steps = set()
+                self.exp_avg.zero_()
+                self.exp_avg_sq.zero_()
+                for idx, st in per_param.items():
+                    p = params[int(idx)]
+                    self._moment_view(self.exp_avg, p).copy_(st["exp_avg"])
+                    self._moment_view(self.exp_avg_sq, p).copy_(st["exp_avg_sq"])
+                    steps.add(int(float(st["step"])))
+                if len(steps) > 1:
+                    raise ValueError(f"FusedAdamW keeps one step count; the state has {sorted(steps)}")
+                self.step_count = steps.pop() if steps else 0
 
     @torch.no_grad()
     def step(self, closure=None, grad_scale: float = 1.0):

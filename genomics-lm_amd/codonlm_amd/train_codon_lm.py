@@ -23,15 +23,14 @@ def main(argv=None):
     ap.add_argument("--config", required=True)
     ap.add_argument("--run_id", default=None, help="Unique run id; falls back to $RUN_ID or config.run_id")
     ap.add_argument("--resume", default=None, help="Path to checkpoint to resume training from")
-    ap.add_argument("--transfer_from", default=None, help="Path to pre-trained weights (not supported here)")
+    ap.add_argument("--transfer_from", default=None,
+                    help="Path to pre-trained weights to initialize model from (ignores optimizer/step state)")
     ap.add_argument("--train_npz", action="append", default=None, help="Training NPZ file (repeatable)")
     ap.add_argument("--val_npz", action="append", default=None, help="Validation NPZ file (repeatable)")
     ap.add_argument("--test_npz", action="append", default=None, help="Test NPZ file (repeatable)")
     ap.add_argument("--save_epochs", action="store_true", help="Save checkpoint at every epoch")
     ap.add_argument("--max_time_minutes", type=float, default=None, help="Override config max_time_minutes")
     args = ap.parse_args(argv)
-    if args.transfer_from:
-        raise NotImplementedError("--transfer_from (vocabulary-adapting warm start) is outside the MI355X hot path")
     with open(args.config) as f:
         cfg = yaml.safe_load(f) or {}
     if "data" in cfg and isinstance(cfg["data"], dict):

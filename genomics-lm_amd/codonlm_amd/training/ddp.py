@@ -17,6 +17,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _lib as L
+from ..model_tiny_gpt import mix_seed_rank
 
 
 def bucket_ranges(model):
@@ -46,7 +47,9 @@ class DataParallelStep:
         self.model = model
         self.opt = optimizer
         self.group = group
-        self.world = dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+        on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(group) if on else 1
+        self.rank = dist.get_rank(group) if on else 0
         self.ranges = bucket_ranges(model)
 
     def _hook(self, handles):
@@ -60,17 +63,24 @@ class DataParallelStep:
                 handles.append(dist.all_reduce(grads[b:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         return hook
 
+    def bucket_hook(self, handles):
+        """engine.backward / TinyGPT._bucket_hook callback that launches the async all-reduces."""
+        return self._hook(handles)
+
     def microbatch(self, idx, targets, *, seed: int, accumulate: bool, sync: bool):
-        """Forward + backward of one microbatch; all-reduce only when ``sync`` (last of a group)."""
+        """Forward + backward of one microbatch; all-reduce only when ``sync`` (last of a group).
+        The rank is mixed into the dropout seed (independent masks per rank)."""
         eng = self.model.engine
-        _, loss = eng.forward(idx, targets, training=True, seed=seed)
+        _, loss = eng.forward(idx, targets, training=True, seed=mix_seed_rank(seed, self.rank))
         handles = []
         eng.backward(accumulate=accumulate, bucket_hook=self._hook(handles) if sync else None)
         return loss, handles
 
-    def step(self, idx, targets, *, seed: int, n_micro: int = 1):
+    def step(self, idx, targets, *, seed: int):
+        """One optimizer step on one microbatch per rank (grad_accum_steps = 1): gradients are
+        averaged over the ranks (1/world folded into AdamW)."""
         loss, handles = self.microbatch(idx, targets, seed=seed, accumulate=False, sync=True)
         for h in handles:
             h.wait()
-        self.opt.step(grad_scale=1.0 / (self.world * n_micro))
+        self.opt.step(grad_scale=1.0 / self.world)
         return loss

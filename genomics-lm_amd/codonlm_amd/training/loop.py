@@ -18,15 +18,25 @@ so runs, resumes and downstream tools interchange:
 * resume (:879-942) skips already-applied microbatches of the interrupted epoch; wall-time
   limit (:1459-1500); metrics.json / meta.json (:1556-1597).
 
+* warm start (loop.py:266,824-877): ``--transfer_from`` or the cfg key ``transfer_from``
+  (ignored on resume) loads a checkpoint with the vocabulary-remapping transfer load
+  (training/checkpoint.py) and records the transfer provenance in vocabulary.json;
+* corrected primary configs (loop.py:174-195) are validated fail-closed
+  (training/primary_contract.py); their pinned ``device: mps`` runs on the MI355X engine.
+
 MI355X-first differences: token stores live in HBM and batches are gathered on the device
 (data_loading.py here); fwd+CE+bwd run in the native engine; with torch.distributed
-initialised each rank takes every world-th batch and the flat gradient buffer is
-all-reduced over RCCL once per committed group (1/world folded into AdamW); loss values
-are read once per microbatch (one host sync) as the reference's isfinite check also does.
+initialised each rank takes every world-th batch, the last microbatch of a group hands the
+bucketed RCCL all-reduce to the backward (each block's gradient range is reduced while the
+blocks below it are still in backward; 1/world folded into AdamW), the nonfinite-abort and
+wall-time decisions are one collective per microbatch over a CPU process group
+(training/stepper.py), and the rank is mixed into the dropout seeds.  Per microbatch the
+host reads the loss values once, through an event recorded after the forward, so the
+backward's kernels keep the GPU busy meanwhile; nothing else synchronises.
 
 Outside the MI355X hot path and rejected with a clear error: shape guidance / biophysics
 encoder, replay-termination loss, Adafactor, freeze_backbone, torch.compile (ignored: the
-engine is already native), dataset manifests / primary-config contracts (not enforced).
+engine is already native), dataset manifests (not enforced).
 """
 from __future__ import annotations
 
@@ -50,6 +60,10 @@ from ..data_loading import DeviceBatchLoader, DeviceCodonDataset
 from ..model_tiny_gpt import TinyGPT
 from ..optim import FusedAdamW
 from . import objectives as obj
+from .checkpoint import load_transfer_state_dict, transfer_source_itos
+from .ddp import DataParallelStep
+from .primary_contract import validate_primary_training_config
+from .stepper import GroupController, control_group
 
 RUN_ID_ENV = "RUN_ID"
 PAD_ID = 0
@@ -260,6 +274,29 @@ def configuration_fingerprint(cfg: dict) -> str:
 
 
 # ------------------------------------------------------------------------------ training
+def resolve_device(cfg: dict, local_rank: int = 0) -> torch.device:
+    """dev() of loop.py:152-170 on the MI355X path: 'auto' / 'cuda' -> this process's GPU;
+    'mps' (pinned by the corrected primary configs) is accepted and runs on the MI355X engine;
+    'cpu' is refused (the engine has no CPU path); anything else is a ValueError as in the
+    reference."""
+    requested = str(cfg.get("device", "auto") or "auto").lower()
+    if requested not in {"auto", "cpu", "mps", "cuda"}:
+        raise ValueError(f"unsupported device {requested!r}; expected auto, cpu, mps, or cuda")
+    if requested == "cpu":
+        raise RuntimeError("device=cpu requested, but the codonlm_amd trainer runs only on the MI355X engine "
+                           "(train on CPU with the reference trainer)")
+    if not torch.cuda.is_available():
+        raise RuntimeError(f"requested device={requested} but no MI355X is visible (the codonlm_amd trainer has "
+                           "no CPU path)")
+    torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+    device = torch.device("cuda", torch.cuda.current_device())
+    if requested == "mps":
+        cfg["device_contract"] = "mps"
+        print(f"[device] device=mps (pinned by the config) -> {device}: the MI355X engine runs the MPS path "
+              "(bf16 MFMA compute instead of fp16 autocast; fp32 master weights, loss and optimizer)")
+    return device
+
+
 def build_model(cfg: dict, device) -> TinyGPT:
     """cfg -> TinyGPT kwargs as loop.py:559-579 (plus compute_dtype)."""
     sep_mask_enabled = bool(cfg.get("sep_mask_enabled", True))
@@ -300,6 +337,16 @@ def _reject_out_of_scope(cfg: dict) -> None:
 
 
 def run_training(cfg: dict, args) -> None:
+    if cfg.get("primary_training_contract") is not None:  # loop.py:174-195
+        contract = validate_primary_training_config(cfg)
+        requested = (getattr(args, "run_id", None) or "").strip()
+        if requested and requested != contract["run_id"]:
+            raise ValueError("--run_id cannot override an immutable primary training config")
+        for name in ("train_npz", "val_npz", "test_npz", "transfer_from"):
+            if getattr(args, name, None) is not None:
+                raise ValueError(f"--{name} cannot override an immutable primary training config")
+        print(f"[contract] corrected primary config verified role={contract['role']} "
+              f"protocol={contract['protocol']} seed={contract['seed']}")
     _reject_out_of_scope(cfg)
     cfg = dict(cfg)
     resume_path = args.resume or cfg.pop("resume", None)
@@ -316,19 +363,22 @@ def run_training(cfg: dict, args) -> None:
     cfg["vocab_size"] = vocab_size
     if resume_path and not os.path.isfile(resume_path):
         raise FileNotFoundError(f"Resume checkpoint not found: {resume_path}")
+    # loop.py:266 -- CLI or cfg, never on resume (the cfg key is consumed either way)
+    cfg_transfer = cfg.pop("transfer_from", None)
+    transfer_path = None if resume_path else (getattr(args, "transfer_from", None) or cfg_transfer)
+    if transfer_path and not os.path.isfile(transfer_path):
+        raise FileNotFoundError(f"Transfer weights not found: {transfer_path}")
 
     # ---- distributed layout (one process per GPU; RCCL = backend "nccl")
     dist_on = dist.is_available() and dist.is_initialized()
     rank = dist.get_rank() if dist_on else 0
     world = dist.get_world_size() if dist_on else 1
-    if torch.cuda.is_available():
-        local = int(os.environ.get("LOCAL_RANK", rank if dist_on else torch.cuda.current_device()))
-        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
-        device = torch.device("cuda", torch.cuda.current_device())
-    else:
-        raise RuntimeError("the codonlm_amd trainer needs an MI355X (no CPU path)")
+    local = int(os.environ.get("LOCAL_RANK", rank if dist_on else
+                               (torch.cuda.current_device() if torch.cuda.is_available() else 0)))
+    device = resolve_device(cfg, local)
     cfg["device"] = str(device)
     is_main = rank == 0
+    ctrl = control_group(world)
 
     base_seed = int(cfg.get("seed", 1337))
     train_ds = DeviceCodonDataset(train_paths, device)
@@ -342,7 +392,8 @@ def run_training(cfg: dict, args) -> None:
                                  n_buckets=int(cfg.get("n_buckets", 8)), rank=rank, world=world)
 
     def val_loader() -> DeviceBatchLoader:
-        return DeviceBatchLoader(val_ds, batch_size, shuffle=False, rank=rank, world=world)
+        # every val batch exactly once over the ranks (sums reduced after the pass)
+        return DeviceBatchLoader(val_ds, batch_size, shuffle=False, rank=rank, world=world, drop_remainder=False)
 
     multi_offset_weights = (normalize_offset_weights([int(x) for x in cfg.get("multi_offset_targets", [])],
                                                      cfg.get("multi_offset_weights"))
@@ -404,6 +455,31 @@ def run_training(cfg: dict, args) -> None:
 
     torch.manual_seed(base_seed)
     model = build_model(cfg, device)
+    model._seed_rank = rank  # independent dropout masks per rank
+    if transfer_path:  # loop.py:824-877
+        if is_main:
+            print(f"[transfer] initializing model from {transfer_path}")
+        ck_t = torch.load(transfer_path, map_location=device, weights_only=True)
+        sd = ck_t["model"] if isinstance(ck_t, dict) and "model" in ck_t else ck_t
+        t_cfg = ck_t.get("cfg", {}) if isinstance(ck_t, dict) else {}
+        source_itos = transfer_source_itos(transfer_path, t_cfg)
+        report = load_transfer_state_dict(model, sd, source_itos=source_itos,
+                                          target_itos=itos if itos is not None else None)
+        src_rows = int(sd["tok_emb.weight"].shape[0]) if "tok_emb.weight" in sd else None
+        cfg["vocabulary"]["legacy_adaptation"] = bool(src_rows != vocab_size or report["loaded_rows"])
+        cfg["vocabulary"]["transfer"] = {"checkpoint": str(transfer_path), "source_embedding_rows": src_rows,
+                                         "source_tokenizer_entries": len(source_itos) if source_itos else None,
+                                         "target_vocab_size": int(vocab_size), "loaded_rows": report["loaded_rows"],
+                                         "skipped": report["skipped"]}
+        if is_main:
+            (run_dir / "vocabulary.json").write_text(json.dumps(cfg["vocabulary"], indent=2, sort_keys=True) + "\n")
+            print(f"[transfer] loaded_exact={len(report['loaded_exact'])} row_loaded={report['loaded_rows']}")
+            if report["skipped"]:
+                print(f"[transfer] skipped_shape_or_missing={report['skipped']}")
+            if report["missing"]:
+                print(f"[transfer] missing_after_adapt={report['missing']}")
+            if report["unexpected"]:
+                print(f"[transfer] unexpected_after_adapt={report['unexpected']}")
     term_cw = (torch.tensor([float(v) for v in term_cw_values], dtype=torch.float32, device=device)
                if term_cw_values is not None else None)
     lr_base = float(cfg.get("lr", 5e-6))
@@ -513,18 +589,19 @@ def run_training(cfg: dict, args) -> None:
         if is_main:
             save_checkpoint_atomic(p, ckpt_dir / name)
 
-    def allreduce_grads() -> None:
-        if world > 1:
-            dist.all_reduce(model.flat_grads(), op=dist.ReduceOp.SUM)
-
-    def any_nonfinite(flag: bool) -> bool:
-        if world == 1:
-            return flag
-        t = torch.tensor([1.0 if flag else 0.0], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return bool(t.item() > 0)
+    dp = DataParallelStep(model, optim) if world > 1 else None
+    wall_limit = cfg.get("max_time_minutes")
+    t_wall0 = time.perf_counter()
+    ctl = GroupController(gacc=gacc, health=accumulation_health, world=world, group=ctrl,
+                          wall_limit_s=float(wall_limit) * 60.0 if wall_limit else None, t0=t_wall0)
+    # class weights of the next-codon loss, once (the reference checks torch.all(w == 1) per step)
+    offset_lw = model.loss_weights if not bool(torch.all(model.loss_weights == 1.0)) else None
+    offset_keys = sorted(multi_offset_weights)
+    stats_host = torch.empty(4 + 2 * len(offset_keys), dtype=torch.float32, pin_memory=True)
 
     def forward_objective(xb, yb):
+        """The trainer's objective (loop.py:1075-1112) as device tensors: (total, next, term or
+        None, {offset: loss}, {offset: n_valid})."""
         need_aux = term_enabled or bool(multi_offset_weights)
         if need_aux:
             logits, next_loss, aux = model(xb, yb, return_aux=True)
@@ -532,23 +609,44 @@ def run_training(cfg: dict, args) -> None:
             logits, next_loss = model(xb, yb)
             aux = {}
         total = next_loss
-        offset_losses = {}
+        offset_losses, offset_counts = {}, {}
         if multi_offset_weights:
-            lw = model.loss_weights if not torch.all(model.loss_weights == 1.0).item() else None
-            off_total, offset_losses = obj.multi_offset_lm_loss(aux.get("offset_logits", logits), yb,
-                                                                multi_offset_weights,
-                                                                label_smoothing=float(cfg.get("label_smoothing", 0.0)),
-                                                                loss_weights=lw)
+            off_total, offset_losses, offset_counts = obj.multi_offset_lm_loss(
+                aux.get("offset_logits", logits), yb, multi_offset_weights,
+                label_smoothing=float(cfg.get("label_smoothing", 0.0)), loss_weights=offset_lw, return_counts=True)
             total = total + off_total
         term_loss = None
         if term_enabled:
             labels = obj.termination_distance_bucket_labels(yb, stop_ids=term_stop_ids, bucket_edges=term_edges)
             term_loss = obj.termination_aux_loss(aux["termination_logits"], labels, class_weights=term_cw)
             total = total + term_weight * term_loss
-        return total, next_loss, offset_losses, term_loss
+        return total, next_loss, term_loss, offset_losses, offset_counts
 
-    wall_limit = cfg.get("max_time_minutes")
-    t_wall0 = time.perf_counter()
+    def read_stats(total, next_loss, term_loss, off_losses, off_counts, yb):
+        """One device->host transfer of the microbatch's scalars, recorded right after the
+        forward: the caller enqueues the backward and then waits on the returned event only,
+        so the backward's kernels run while the host decides."""
+        parts = [total.detach().float().reshape(1), next_loss.detach().float().reshape(1),
+                 (term_loss.detach().float() if term_loss is not None else torch.zeros((), device=device)).reshape(1),
+                 yb.ne(PAD_ID).sum().reshape(1).float()]
+        for k in offset_keys:
+            parts.append(off_losses[k].detach().float().reshape(1) if k in off_losses
+                         else torch.zeros(1, device=device))
+            parts.append(off_counts[k].float().reshape(1) if k in off_counts else torch.zeros(1, device=device))
+        host = stats_host[: len(parts)]
+        host.copy_(torch.cat(parts), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host, ev
+
+    def unpack(host):
+        v = host.tolist()
+        total, nxt, term, ntok = v[0], v[1], v[2], v[3]
+        offs = {}
+        for i, k in enumerate(offset_keys):  # offsets without a valid target are skipped
+            if v[5 + 2 * i] > 0:
+                offs[k] = v[4 + 2 * i]
+        return total, nxt, term, int(round(ntok)), offs
 
     def one_pass(split, loader, epoch_idx, skip=0):
         train = split == "train"
@@ -564,23 +662,30 @@ def run_training(cfg: dict, args) -> None:
         optim.zero_grad(set_to_none=True)
         skipped = 0
         health_before = accumulation_health.state_dict()
-        pending_tok = torch.zeros((), dtype=torch.int64, device=device)
+        pending = {"tok": 0}
+        handles: list = []
+
+        def drain():
+            for h in handles:
+                h.wait()
+            handles.clear()
 
         def step_optimizer(group_size: int, batch_idx: int) -> None:
             if group_size <= 0:
                 return
-            allreduce_grads()
+            if world > 1:
+                if handles:
+                    drain()  # the buckets were all-reduced during this microbatch's backward
+                else:
+                    dist.all_reduce(model.flat_grads(), op=dist.ReduceOp.SUM)
             if (not use_cosine) and warmup_steps > 0 and st.step < warmup_steps:
                 for pg in optim.param_groups:
                     pg["lr"] = base_lr * float(st.step + 1) / max(1, warmup_steps)
             optim.step(grad_scale=1.0 / (group_size * world))
             optim.zero_grad(set_to_none=True)
             accumulation_health.complete_group()
-            tok = pending_tok.clone()
-            if world > 1:
-                dist.all_reduce(tok, op=dist.ReduceOp.SUM)
-            st.consumed += int(tok.item())
-            pending_tok.zero_()
+            st.consumed += int(round(ctl.sum([pending["tok"]])[0]))
+            pending["tok"] = 0
             for k in ("total_loss_sum", "next_loss_sum", "microbatches"):
                 epoch_metrics[k] += pending_metrics[k]
             if epoch_metrics["initial_loss"] is None:
@@ -591,6 +696,7 @@ def run_training(cfg: dict, args) -> None:
             if use_cosine:
                 scheduler.step()
 
+        shard = len(loader)
         batch_idx = -1
         for batch_idx, (xb, yb) in enumerate(loader):
             st.cur_epoch = epoch_idx
@@ -599,13 +705,26 @@ def run_training(cfg: dict, args) -> None:
                 continue
             st.cur_mb = batch_idx + 1
             with torch.set_grad_enabled(train):
-                loss, next_loss, off_losses, term_loss = forward_objective(xb, yb)
-            vals = torch.stack([loss.detach().float(), next_loss.detach().float()]).tolist()  # one host sync
-            if any_nonfinite(not math.isfinite(vals[0])):  # torch.isfinite(loss), loop.py:1197
+                loss, next_loss, term_loss, off_losses, off_counts = forward_objective(xb, yb)
+            host, ev = read_stats(loss, next_loss, term_loss, off_losses, off_counts, yb)
+            if train:
+                # backward enqueued before the finiteness verdict: a nonfinite microbatch aborts
+                # its whole group, whose gradients are then discarded anyway (loop.py:1197-1219)
+                if dp is not None and ctl.completes_group(batch_idx == shard - 1):
+                    model._bucket_hook = dp.bucket_hook(handles)
+                loss.backward()
+            ev.synchronize()
+            vals = unpack(host)
+            if train:
+                abort, stop = ctl.agree(not math.isfinite(vals[0]))
+            else:
+                abort, stop = not math.isfinite(vals[0]), False
+            if abort:  # torch.isfinite(loss), loop.py:1197
                 skipped += 1
                 if train:
+                    drain()
                     discarded = accumulation_health.abort_group(optim)
-                    pending_tok.zero_()
+                    pending["tok"] = 0
                     pending_metrics.update(total_loss_sum=0.0, next_loss_sum=0.0, microbatches=0, initial_loss=None)
                     st.cur_resume_mb = batch_idx + 1
                     if is_main:
@@ -618,26 +737,26 @@ def run_training(cfg: dict, args) -> None:
                             f"{max_nonfinite_groups}: {accumulation_health.aborted_groups}")
                 continue
             stepped = False
+            v_total, v_next, v_term, ntok, v_offs = vals
             if train:
                 if epoch_metrics["initial_loss"] is None and pending_metrics["initial_loss"] is None:
-                    pending_metrics["initial_loss"] = vals[0]
-                pending_metrics["total_loss_sum"] += vals[0]
-                pending_metrics["next_loss_sum"] += vals[1]
+                    pending_metrics["initial_loss"] = v_total
+                pending_metrics["total_loss_sum"] += v_total
+                pending_metrics["next_loss_sum"] += v_next
                 pending_metrics["microbatches"] += 1
-                loss.backward()
-                pending_tok += yb.ne(PAD_ID).sum()
+                pending["tok"] += ntok
                 accumulation_health.record_finite_microbatch()
                 if accumulation_health.active_microbatches == gacc:
                     step_optimizer(accumulation_health.active_microbatches, batch_idx)
                     stepped = True
             else:
-                total += vals[0]
-                next_total += vals[1]
+                total += v_total
+                next_total += v_next
             if term_loss is not None:
-                term_total += float(term_loss.detach().item())
+                term_total += v_term
                 term_count += 1
-            for o, ol in off_losses.items():
-                off_tot[o] += float(ol.detach().item())
+            for o, val in v_offs.items():
+                off_tot[o] += val
                 off_cnt[o] += 1
             n += 1
             if stepped and is_main and (
@@ -647,18 +766,18 @@ def run_training(cfg: dict, args) -> None:
                 p["checkpoint_reason"] = "periodic"
                 save(p, "last.pt")
                 last_saved.update(step=st.step, t=time.monotonic())
-            if wall_limit and time.perf_counter() - t_wall0 > float(wall_limit) * 60.0:
+            if stop:
                 raise WallTimeLimitException()
         if train and accumulation_health.active_microbatches:
             step_optimizer(accumulation_health.active_microbatches, batch_idx)
+        drain()
         if train:
             total, next_total, n = (float(epoch_metrics["total_loss_sum"]), float(epoch_metrics["next_loss_sum"]),
                                     int(epoch_metrics["microbatches"]))
         elif world > 1:
-            red = torch.tensor([total, next_total, float(n), term_total, float(term_count)], dtype=torch.float64,
-                               device=device)
-            dist.all_reduce(red, op=dist.ReduceOp.SUM)
-            total, next_total, n, term_total, term_count = red.tolist()
+            total, next_total, n, term_total, term_count = ctl.sum([total, next_total, n, term_total, term_count])
+            for o in off_tot:
+                off_tot[o], off_cnt[o] = ctl.sum([off_tot[o], off_cnt[o]])
         offset_avgs = {o: off_tot[o] / max(off_cnt[o], 1) for o in off_tot}
         health_after = accumulation_health.state_dict()
         return (total / max(n, 1), next_total / max(n, 1),

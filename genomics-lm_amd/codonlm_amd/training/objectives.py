@@ -63,9 +63,16 @@ def multi_offset_lm_loss(
     label_smoothing: float = 0.0,
     loss_weights: torch.Tensor | None = None,
     boundary_ids=DEFAULT_BOUNDARY_IDS,
+    return_counts: bool = False,
 ):
-    """sum_k w_k CE(logits_k at t, y[t+k-1]) over the valid targets (objectives.py:26-60)."""
+    """sum_k w_k CE(logits_k at t, y[t+k-1]) over the valid targets (objectives.py:26-60).
+
+    The reference skips an offset with no valid target (a host-side ``valid.any()``).
+    ``return_counts=True`` keeps that decision on the device: an empty offset adds 0 to the
+    total (its CE is 0/0; the gradient it passes is 0) and its entry in ``losses`` must be
+    ignored by the caller when ``counts[k] == 0`` -- (total, losses, counts), no host sync."""
     losses = {}
+    counts = {}
     total = torch.zeros((), dtype=torch.float32, device=yb.device)
     T = yb.shape[1]
     for offset, weight in offset_weights.items():
@@ -78,13 +85,18 @@ def multi_offset_lm_loss(
         else:
             pred = logits
         tk, n_valid = ops.offset_targets(yb, offset, boundary_ids)
-        if int(n_valid.item()) == 0:  # the reference's bool(valid.any()) host check
+        if not return_counts and int(n_valid.item()) == 0:  # the reference's bool(valid.any())
             continue
         V = pred.shape[-1]
         offset_loss = cross_entropy(pred[:, :T].reshape(-1, V), tk.view(-1), ignore_index=PAD_ID,
                                     label_smoothing=label_smoothing, weight=loss_weights)
         losses[offset] = offset_loss
+        if return_counts:
+            counts[offset] = n_valid
+            offset_loss = torch.where(n_valid.reshape(()) > 0, offset_loss, torch.zeros_like(offset_loss))
         total = total + (float(weight) * offset_loss)
+    if return_counts:
+        return total, losses, counts
     return total, losses
 
 

@@ -606,7 +606,7 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   if (m->cfg.use_rope && (!m->rope_cos || !m->rope_sin)) return CG_EINVAL;
   m->B = B; m->T = T; m->training = training; m->seed = seed; m->window = window;
   m->idx = idx; m->targets = targets;
-  m->aux_ready = 0; m->head_grad_scale = 1.0f;
+  m->aux_ready = 0; m->head_grad_scale = 1.0f; m->head_grad_scale_dev = nullptr;
   m->d_term_logits = nullptr; m->ld_d_term = 0;
   for (int i = 0; i < 8; ++i) m->d_offset_logits[i] = nullptr;
   Ctx C;
@@ -731,6 +731,9 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
     CK(fill_head2(C, hoff));
+    if (m->targets && m->head_grad_scale_dev)  // d(objective)/d(loss) still on the device
+      CK(cg_scale_dev(C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, (int)M, D.Vp, m->head_grad_scale_dev,
+                      C.s));
     if (m->targets) {
       // d(head weight) = s dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero; the hi
       // half of split-bf16 rows)

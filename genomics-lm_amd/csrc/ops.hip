@@ -1195,6 +1195,44 @@ extern "C" int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n,
   return CG_OK;
 }
 
+// x[r][c] *= *s for a gradient buffer (dtype F32 / BF16 / BF16X2 split pairs, ld in elements;
+// BF16X2 rows hold hi in [0, ld/2) and lo in [ld/2, ld)).  The scale is read on the device (the
+// autograd output gradient d(objective)/d(loss)), so no host synchronisation is needed; a
+// scale of exactly 1 returns at once.
+__global__ __launch_bounds__(256) void scale_dev_kernel(int dtype, void* __restrict__ x, long long ld, int rows,
+                                                        int cols, const float* __restrict__ sp) {
+  const float sc = *sp;
+  if (sc == 1.0f) return;
+  const long long total = (long long)rows * cols;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long r = i / cols;
+    const int c = (int)(i - r * cols);
+    if (dtype == CG_F32) {
+      float* p = (float*)x + r * ld + c;
+      *p *= sc;
+    } else if (dtype == CG_BF16) {
+      bf16_t* p = (bf16_t*)x + r * ld + c;
+      *p = f2bf(bf2f(*p) * sc);
+    } else {
+      bf16_t* p = (bf16_t*)x + r * ld;
+      const float v = (bf2f(p[c]) + bf2f(p[ld / 2 + c])) * sc;
+      st_grad<bf16_t, true>(p, c, ld / 2, v);
+    }
+  }
+}
+extern "C" int cg_scale_dev(int dtype, void* x, long long ld, int rows, int cols, const float* scale, void* stream) {
+  if (!x || !scale || rows < 0 || cols < 0) return CG_EINVAL;
+  if (dtype != CG_F32 && dtype != CG_BF16 && dtype != CG_BF16X2) return CG_EINVAL;
+  if (ld < (dtype == CG_BF16X2 ? 2LL * cols : cols)) return CG_EINVAL;
+  const long long total = (long long)rows * cols;
+  if (!total) return CG_OK;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(scale_dev_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dtype, x, ld, rows, cols, scale);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
 // fp32 [rows][cols] -> dtype [rows][dcols] with zero pad columns (aux-head logit grads into
 // the padded GEMM operand layout)
 template <typename T_, bool SPLIT = false>

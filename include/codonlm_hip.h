@@ -192,6 +192,8 @@ int cg_transpose16_batch(const cg_transpose_batch* tb, void* stream);
 /* elementwise casts / utilities */
 int cg_cast_f32_to_bf16(const float* src, uint16_t* dst, long long n, void* stream);
 int cg_cast_bf16_to_f32(const uint16_t* src, float* dst, long long n, void* stream);
+/* x[r][c] *= *scale (device float; exactly 1 is a no-op) for dtype CG_F32 / CG_BF16 / CG_BF16X2 */
+int cg_scale_dev(int dtype, void* x, long long ld, int rows, int cols, const float* scale, void* stream);
 /* dst[r][c] = src[r][c] (c < cols), 0 for cols <= c < dcols; dst in `dtype` (CG_BF16X2: hi in
  * columns [0, dcols), lo in [dcols, 2 dcols); ldd >= 2 dcols) */
 int cg_cast_pad_2d(const float* src, long long lds, int rows, int cols, int dtype, void* dst,
@@ -296,6 +298,7 @@ typedef struct {
    * cg_model_aux_forward and cg_model_backward phase 0. */
   int aux_ready;                    /* set by cg_model_aux_forward                      */
   float head_grad_scale;            /* d(objective)/d(next-codon loss)                  */
+  const float* head_grad_scale_dev; /* optional device float multiplying it (no host sync) */
   const float* d_term_logits;       /* fp32 [B*T][ld_d_term] or NULL                    */
   long long ld_d_term;
   const float* d_offset_logits[8];  /* fp32 [B*T][V] per offset head, or NULL           */

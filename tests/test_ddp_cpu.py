@@ -3,7 +3,7 @@
 DataParallelStep's buckets must tile the flat gradient buffer exactly (each backward phase
 of the native engine completes one contiguous range), every bucket must be all-reduced
 once per optimizer step right after its phase is enqueued, and the optimizer must see the
-rank-average (grad_scale = 1/(world*n_micro)).  The native engine is replaced by a CPU
+rank-average (grad_scale = 1/world).  The native engine is replaced by a CPU
 stand-in that writes rank-dependent gradients phase by phase.
 """
 import os
@@ -62,7 +62,7 @@ def _worker(rank, world, port, out):
         m._engine = _FakeEngine(m, rank, log)
         opt = _FakeOpt()
         step = DataParallelStep(m, opt)
-        step.step(None, None, seed=0, n_micro=2)
+        step.step(None, None, seed=0)
         # coverage: buckets tile [0, total) without overlap
         rng = bucket_ranges(m)
         spans = sorted(rng.values())
@@ -87,5 +87,5 @@ def test_ddp_buckets_allreduce_gloo():
     for r in range(world):
         ok, scales, log = out[r]
         assert ok, f"rank {r}: gradients are not the rank-sum"
-        assert scales == [pytest.approx(1.0 / (world * 2))]
+        assert scales == [pytest.approx(1.0 / world)]
         assert log[0] == "head" and log[-1] == "embed" and log[1:-1] == [2, 1, 0]

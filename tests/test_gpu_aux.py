@@ -166,8 +166,14 @@ def test_scaled_loss_and_aux_only_backward():
     m.zero_grad()
     _, loss = m(x, y)
     (2.5 * loss).backward()
+    # the scale d(2.5 loss)/d(loss) is applied on the device to the head gradient before the
+    # backward products: equal up to fp32 rounding of the scaled operands
     for k, p in m.named_parameters():
-        torch.testing.assert_close(p.grad, 2.5 * ref[k], rtol=1e-5, atol=1e-7, msg=k)
+        # (key biases' exact gradient is 0 -- softmax shift invariance -- so they hold rounding
+        # noise only: compared at the query bias' scale)
+        sk = k.replace("key.bias", "query.bias") if k.endswith("attn.key.bias") else k
+        atol = 2e-6 * float(ref[sk].abs().max()) + 1e-12
+        torch.testing.assert_close(p.grad, 2.5 * ref[k], rtol=1e-5, atol=atol, msg=k)
     # aux-only objective (no targets): termination loss alone
     m.zero_grad()
     _, none_loss, aux = m(x, return_aux=True)

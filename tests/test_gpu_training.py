@@ -196,3 +196,45 @@ def test_end_to_end_run_with_aux_heads(tmp_path, monkeypatch):
     from codonlm_amd.training.loop import build_model
     m = build_model(dict(ck["cfg"]), DEV)
     m.load_state_dict(ck["model"])
+
+
+def test_transfer_from_cfg_remaps_vocabulary_and_runs(tmp_path, monkeypatch):
+    """stage2.6_large_scaling-style warm start (configs/stage2.6_large_scaling.yaml:16): the cfg
+    key transfer_from loads a previous run's checkpoint into a deeper model with a different
+    vocabulary through the reference's row remapping (training/checkpoint.py:16-85,
+    loop.py:266,824-877); device: mps (the primary contracts' pin) runs on the MI355X."""
+    from codonlm_amd.training.loop import run_training
+    monkeypatch.chdir(tmp_path)
+    rng = np.random.default_rng(2)
+    T = 32
+    seq = rng.integers(4, 68, size=(12, T + 1)).astype(np.int32)
+    src_cfg = _config(tmp_path, vocab_size=69, block_size=T, n_layer=1, n_head=1, batch_size=4, grad_accum_steps=1,
+                      epochs=1, compute_dtype="bf16")
+    config_path, paths = _write_inputs(tmp_path, src_cfg, seq[:8, :-1], seq[:8, 1:], seq[8:, :-1], seq[8:, 1:], V=69)
+    run_training(dict(src_cfg), _args(config_path, paths, run_id="src-run"))
+    src_ck = tmp_path / "runs/src-run/checkpoints/last.pt"
+    src = torch.load(src_ck, map_location="cpu", weights_only=True)["model"]
+    # target: 68 tokens with the source's token_5 / token_6 swapped and token_7 renamed, 2 layers
+    tgt_dir = tmp_path / "tgt"
+    tgt_dir.mkdir()
+    itos = [f"token_{i}" for i in range(68)]
+    itos[5], itos[6], itos[7] = "token_6", "token_5", "novel"
+    (tgt_dir / "itos.txt").write_text("\n".join(itos) + "\n")
+    tgt_cfg = _config(tgt_dir, vocab_size=68, block_size=T, n_layer=2, n_head=1, batch_size=4, grad_accum_steps=1,
+                      epochs=1, compute_dtype="bf16", lr=0.0, min_lr=0.0, device="mps",
+                      transfer_from=str(src_ck), itos_path=str(tgt_dir / "itos.txt"))
+    tgt_cfg_path = tgt_dir / "config.yaml"
+    tgt_cfg_path.write_text(yaml.safe_dump(tgt_cfg))
+    run_training(dict(tgt_cfg), _args(tgt_cfg_path, paths, run_id="tgt-run"))
+    ck = torch.load(tmp_path / "runs/tgt-run/checkpoints/last.pt", map_location="cpu", weights_only=True)
+    emb, semb = ck["model"]["tok_emb.weight"], src["tok_emb.weight"]
+    # lr 0: the trained weights are exactly the transferred ones
+    assert torch.equal(emb[5], semb[6]) and torch.equal(emb[6], semb[5]) and torch.equal(emb[20], semb[20])
+    assert not torch.equal(emb[7], semb[7])
+    assert torch.equal(ck["model"]["blocks.0.attn.query.weight"], src["blocks.0.attn.query.weight"])
+    voc = ck["cfg"]["vocabulary"]
+    assert voc["legacy_adaptation"] is True and voc["transfer"]["source_embedding_rows"] == 69
+    assert "tok_emb.weight:67" in voc["transfer"]["loaded_rows"]
+    assert json.loads((tmp_path / "runs/tgt-run/vocabulary.json").read_text())["transfer"]["checkpoint"] == str(src_ck)
+    assert ck["cfg"]["device_contract"] == "mps" and ck["cfg"]["device"].startswith("cuda")
+    assert "transfer_from" not in ck["cfg"]  # consumed like the reference's cfg.pop
