@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Throughput of the MI355X codon-LM training step (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c2|c3|c5] [--path engine|trainer]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Workload = BASELINE config C4: TinyGPT 12L8H d512 (hd 64), T=1024, V=68 codons, GELU MLP,
@@ -9,12 +9,21 @@ SEP-segment causal mask, dropout 0.1, label smoothing 0.05, bf16 compute with fp
 master weights / AdamW, per-GPU microbatch B=16 (weak scaling), synthetic random codon
 batches already resident in HBM.  One step = fwd + CE + bwd + (RCCL all-reduce) + AdamW.
 Rank 0 prints ONE JSON line.
+
+--path engine (default): the DataParallelStep sequence (native engine calls, bucketed
+RCCL all-reduce during the backward).  --path trainer: the per-microbatch sequence of
+codonlm_amd.training.loop (model(xb, yb) through the nn.Module API, loss.backward()
+through autograd, the stats read behind an event, the rank-consistent group control,
+FusedAdamW + LambdaLR), i.e. what `python -m codonlm_amd.train_codon_lm` runs per step.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import platform
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -28,7 +37,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 CONFIGS = {
-    # BASELINE.json configs[3] (the metric's config); others are parity-test shapes
+    # BASELINE.json configs[3] (the metric's config); the others are the remaining GPU configs
     "c4": dict(n_layer=12, n_head=8, n_embd=512, block_size=1024, batch=16, swiglu=False, rope=False, kv=None),
     "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, batch=64, swiglu=False, rope=False, kv=None),
     "c3": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=64, swiglu=True, rope=True, kv=4),
@@ -37,6 +46,8 @@ CONFIGS = {
     "c5": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=32, swiglu=False, rope=False, kv=None,
                offsets=(2, 4, 8, 16, 32), term=True),
 }
+# CPU-baseline batch per BASELINE.md §3 (the reference's default per-device batch)
+CPU_BATCH = {"c4": 2, "c2": 4, "c3": 4, "c5": 4}
 PEAK_BF16_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
 PEAK_HBM_GBS = 8000.0
 
@@ -67,30 +78,70 @@ def probe_pass(kind, run, first, n):
     return w.value, ms.value, k.value
 
 
-def cpu_baseline(c):
-    """fp32 CPU restatement of the same step (oracle.CpuTrainer), bounded sample, rank 0 only."""
+def _cpu_share():
+    """Host threads this process may use: its affinity set, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, math.floor(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg_name, c, budget_s=25.0):
+    """The fp32 CPU restatement of the same training step (oracle.CpuTrainer: fwd + CE + bwd +
+    AdamW, pinned to the reference), BASELINE.md §3 protocol: the reference's default per-device
+    batch, synthetic codons from default_rng(1337), 20 warmup + 100 measured steps -- both
+    bounded by a time budget (the counts run are reported), on every host thread this process
+    may use.  Rank 0 only."""
     from oracle import tinygpt_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
-    threads = max(1, min(threads, 16))
+    threads = _cpu_share()
     torch.set_num_threads(threads)
     cfg = O.OracleConfig(vocab_size=68, block_size=c["block_size"], n_layer=c["n_layer"], n_head=c["n_head"],
                          n_embd=c["n_embd"], n_kv_head=c["kv"], use_swiglu=c["swiglu"], use_rope=c["rope"],
                          dropout=0.1, label_smoothing=0.05)
     tr = O.CpuTrainer(cfg, O.synthetic_params(cfg, seed=1), lr=3e-4, wd=0.05)
-    Bc, T = 2, c["block_size"]
+    Bc, T = CPU_BATCH[cfg_name], c["block_size"]
     rng = np.random.default_rng(1337)
     tok = rng.integers(4, 68, size=(Bc, T + 1))
     x, y = tok[:, :-1], tok[:, 1:]
-    tr.step(x, y, dropout_seed=1)  # warmup
-    n, t0 = 0, time.perf_counter()
-    while n < 3 or (time.perf_counter() - t0) < 10.0:
-        tr.step(x, y, dropout_seed=2 + n)
-        n += 1
-        if time.perf_counter() - t0 > 30.0:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": n * Bc * T / dt, "unit": "tokens/s", "cores": threads, "kind": "port",
-            "sample": f"{n} fp32 steps of the same model at B={Bc}, T={T} (reference default per-device batch)"}
+    t0 = time.perf_counter()
+    nw = 0
+    while nw < 20 and (nw == 0 or time.perf_counter() - t0 < 0.2 * budget_s):
+        tr.step(x, y, dropout_seed=nw)
+        nw += 1
+    times = []
+    t1 = time.perf_counter()
+    while len(times) < 100 and (len(times) < 2 or time.perf_counter() - t1 < 0.8 * budget_s):
+        s = time.perf_counter()
+        tr.step(x, y, dropout_seed=1000 + len(times))
+        times.append(time.perf_counter() - s)
+    step = float(np.mean(times))
+    return {"value": Bc * T / step, "unit": "tokens/s", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(), "host_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "warmup": nw, "measured": len(times), "ms_per_step": round(step * 1e3, 1),
+            "sample": f"{len(times)} timed fp32 steps (after {nw} warmup) of the same model at B={Bc}, T={T} "
+                      f"(the reference's default per-device batch, BASELINE.md §3), {threads} threads"}
+
+
+def _head():
+    try:
+        return subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip() or None
+    except Exception:
+        return None
 
 
 def main():
@@ -99,6 +150,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--path", default="engine", choices=["engine", "trainer"])
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -129,50 +181,79 @@ def main():
     if world > 1:  # identical replicas
         dist.broadcast(model.flat_parameters(), 0)
     model.train()
+    model._seed_rank = rank
     opt = FusedAdamW(model, lr=3e-4, weight_decay=0.05)
     stepper = DataParallelStep(model, opt)
 
     rng = np.random.default_rng(1337 + rank)
     nbuf = 4
     batches = []
-    for _ in range(nbuf):
+    for j in range(nbuf):
         tok = rng.integers(4, 68, size=(B, T + 1))
-        xb = torch.from_numpy(tok[:, :-1].copy()).to(dev)
-        yb = torch.from_numpy(tok[:, 1:].copy()).to(dev)
-        batches.append((xb, yb))
-
-    def run(i):
-        xb, yb = batches[i % nbuf]
-        return stepper.step(xb, yb, seed=1000 + i)
-
-    if aux:  # the trainer's objective through the model API (aux heads + objectives.py mirror)
-        from codonlm_amd.training import objectives as obj
-        offw = {k: 1.0 / len(c["offsets"]) for k in c.get("offsets", ())}
-        for j, (xb, yb) in enumerate(batches):  # packed segments: BOS ... EOS, SEP every ~330 tokens
-            tok = torch.cat([xb[:, :1], yb], 1)
+        if aux:  # packed segments: BOS ... EOS, SEP every ~330 tokens
             tok[:, 0] = 1
-            for p0 in range(330 + j, T, 330):
+            for p0 in range(330 + j, T + 1, 330):
                 tok[:, p0 - 1], tok[:, p0] = 2, 3
                 if p0 + 1 <= T:
                     tok[:, p0 + 1] = 1
-            batches[j] = (tok[:, :-1].contiguous(), tok[:, 1:].contiguous())
+        batches.append((torch.from_numpy(tok[:, :-1].copy()).to(dev), torch.from_numpy(tok[:, 1:].copy()).to(dev)))
 
-        def run(i):  # noqa: F811
+    from codonlm_amd.training import objectives as obj
+    offw = {k: 1.0 / len(c["offsets"]) for k in c.get("offsets", ())}
+
+    def objective(xb, yb):
+        """The trainer's objective (loop.py:1075-1112) through the model API."""
+        if not aux:
+            _, loss = model(xb, yb)
+            return loss
+        _, loss, auxo = model(xb, yb, return_aux=True)
+        total = loss
+        if offw:
+            off_total, _, _ = obj.multi_offset_lm_loss(auxo["offset_logits"], yb, offw, label_smoothing=0.05,
+                                                       return_counts=True)
+            total = total + off_total
+        if c.get("term"):
+            labels = obj.termination_distance_bucket_labels(yb, stop_ids=(2,))
+            total = total + 0.1 * obj.termination_aux_loss(auxo["termination_logits"], labels)
+        return total
+
+    if args.path == "engine" and not aux:
+        def run(i):
             xb, yb = batches[i % nbuf]
-            opt.zero_grad()
-            _, loss, auxo = model(xb, yb, return_aux=True)
-            total = loss
-            if offw:
-                off_total, _ = obj.multi_offset_lm_loss(auxo["offset_logits"], yb, offw, label_smoothing=0.05)
-                total = total + off_total
-            if c.get("term"):
-                labels = obj.termination_distance_bucket_labels(yb, stop_ids=(2,))
-                total = total + 0.1 * obj.termination_aux_loss(auxo["termination_logits"], labels)
-            total.backward()
+            return stepper.step(xb, yb, seed=1000 + i)
+    else:
+        # the trainer's per-microbatch sequence (training/loop.py one_pass, gacc = 1)
+        from codonlm_amd.training.loop import AccumulationHealth, cosine_lr_lambda
+        from codonlm_amd.training.stepper import GroupController, control_group
+        health = AccumulationHealth()
+        ctl = GroupController(gacc=1, health=health, world=world, group=control_group(world))
+        sched = torch.optim.lr_scheduler.LambdaLR(opt, cosine_lr_lambda(10, 10 ** 6, 3e-4, 3e-5))
+        host = torch.empty(2, dtype=torch.float32, pin_memory=True)
+
+        def run(i):
+            xb, yb = batches[i % nbuf]
+            opt.zero_grad(set_to_none=True)
+            loss = objective(xb, yb)
+            host.copy_(torch.stack([loss.detach().float(), yb.ne(0).sum().float()]), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            handles = []
             if world > 1:
-                dist.all_reduce(model.flat_grads())
+                model._bucket_hook = stepper.bucket_hook(handles)
+            loss.backward()
+            ev.synchronize()
+            v = host.tolist()
+            abort, _ = ctl.agree(not math.isfinite(v[0]))
+            for h in handles:
+                h.wait()
+            if abort:
+                health.abort_group(opt)
+                return loss
+            health.record_finite_microbatch()
             opt.step(grad_scale=1.0 / world)
-            return total
+            health.complete_group()
+            sched.step()
+            return loss
 
     for i in range(args.warmup):
         loss = run(i)
@@ -183,13 +264,13 @@ def main():
     dominant = 0
     if not args.no_kernel_roofline and args.dtype == "bf16":
         nxt = args.warmup
-        for kind in (L.PROBE_GEMM_DW, L.PROBE_GEMM_FWD, L.PROBE_GEMM_DX, L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ,
-                     L.PROBE_ATTN_DKDV):
+        for kind in (L.PROBE_GEMM_DW_GROUPED, L.PROBE_GEMM_DW, L.PROBE_GEMM_FWD, L.PROBE_GEMM_DX, L.PROBE_ATTN_FWD,
+                     L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV):
             probes[kind] = probe_pass(kind, run, nxt, 2)
             nxt += 2
         # roofline candidates are single kernels (one rocprof row each); the fwd/dX GEMM classes
         # span several epilogue specialisations and are reported under "kernels" only
-        single = (L.PROBE_GEMM_DW, L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV)
+        single = tuple(L.PROBE_KERNELS)
         dominant = max(single, key=lambda k: probes[k][1])
         if world > 1:  # all ranks probe the same kernel in the timed region
             t = torch.tensor([dominant], device=dev)
@@ -198,8 +279,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # live HIP events around that kernel's launches in the timed region, 1 launch in 4 (the
-    # 49-launch/step dW sequence shifts phase every step, so all shapes are sampled evenly)
+    # live HIP events around that kernel's launches in the timed region, 1 launch in 4
     L.lib.cg_probe_sample(4)
     L.lib.cg_probe_enable(dominant)
     t0 = time.perf_counter()
@@ -240,10 +320,11 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (uniform random codons 4..67, resident in HBM; random-init weights)",
-        "config": {"workload": f"TinyGPT {c['n_layer']}L{c['n_head']}H d{c['n_embd']} T{T} V68 train step",
+        "config": {"workload": f"TinyGPT {c['n_layer']}L{c['n_head']}H d{c['n_embd']} T{T} V68 train step"
+                               + (" + 5 offset heads + termination head (trainer objective)" if aux else ""),
                    "model": "TinyGPT (genomics-lm src/codonlm)", "global_batch": world * B, "seq_len": T,
                    "micro_batch_per_gpu": B, "parallelism": f"dp{world}", "dropout": 0.1,
-                   "label_smoothing": 0.05, "sep_mask": True},
+                   "label_smoothing": 0.05, "sep_mask": True, "path": args.path if not aux else "trainer"},
         "final_loss": round(final_loss, 4),
         "model_flops_per_token": ftok,
         "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),
@@ -257,20 +338,23 @@ def main():
                               "measured": "HIP events on the launch stream around 1 in 4 launches of the kernel in "
                                           "the timed region"}
         # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
-        # (profiles/<round>/pmc_traffic.json; FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections)
-        tr = ROOT / "profiles" / "round1" / "pmc_traffic.json"
-        if tr.exists() and args.config == "c4" and (B == CONFIGS["c4"]["batch"]):
+        # (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections); attached only for the same config,
+        # batch and kernel, with the commit the counters were collected at
+        tr = ROOT / "profiles" / "round2" / f"pmc_traffic_{args.config}.json"
+        if tr.exists() and B == CONFIGS[args.config]["batch"]:
             t = json.loads(tr.read_text())
             if t.get("probe") == L.PROBE_NAMES[dominant]:
                 result["roofline"]["traffic"] = t["hbm_bytes_per_launch"]
                 result["roofline"]["traffic_unit"] = "HBM bytes/launch (PMC)"
-                result["roofline"]["traffic_source"] = "profiles/round1/pmc_traffic.json"
+                result["roofline"]["traffic_source"] = (f"profiles/round2/pmc_traffic_{args.config}.json "
+                                                        f"(collected at {t.get('commit')}; this run {_head()})")
+                result["roofline"]["traffic_algorithmic"] = t.get("algorithmic_bytes_per_launch")
         result["kernels"] = {
             L.PROBE_NAMES[kk]: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None,
                                 "ms_per_step": round(v[1] / 2, 3), "launches_per_step": v[2] // 2}
-            for kk, v in probes.items()}
+            for kk, v in probes.items() if v[2]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(c)
+        result["cpu_baseline"] = cpu_baseline(args.config, c)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

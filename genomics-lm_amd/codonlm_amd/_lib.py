@@ -19,10 +19,14 @@ LIB_PATH = Path(os.environ.get("CG_LIB_PATH") or Path(__file__).resolve().parent
 CG_F32, CG_BF16, CG_BF16X2 = 0, 1, 2
 CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1, 2, 4, 8, 16, 32, 64
-PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV = range(7)
+(PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV,
+ PROBE_GEMM_DW_GROUPED) = range(8)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
                PROBE_ATTN_FWD: "attn_fwd_mfma", PROBE_ATTN_DQ: "attn_bwd_dq_mfma",
-               PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma"}
+               PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma", PROBE_GEMM_DW_GROUPED: "gemm_dw_grouped"}
+# rocprofv3 kernel-name prefixes of the probed kernels (bench.py matches profiles against them)
+PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: "gemm_dw_kernel", PROBE_ATTN_FWD: "attn_fwd_mfma",
+                 PROBE_ATTN_DQ: "attn_bwd_dq_mfma", PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma"}
 
 # parameter kinds (enum in the header)
 (P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,

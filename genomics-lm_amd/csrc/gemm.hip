@@ -722,9 +722,9 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
   double flops = 0;
   for (int i = 0; i < P.nprod; ++i) flops += 2.0 * P.p[i].N_out * (double)P.p[i].K_out * P.K;
-  cg_probe_begin(CG_PROBE_GEMM_DW, s);
+  cg_probe_begin(CG_PROBE_GEMM_DW_GROUPED, s);
   hipLaunchKernelGGL((gemm_dw_kernel<BM, NS>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
-  cg_probe_end(CG_PROBE_GEMM_DW, s, flops);
+  cg_probe_end(CG_PROBE_GEMM_DW_GROUPED, s, flops);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }

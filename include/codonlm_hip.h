@@ -369,7 +369,8 @@ enum {
   CG_PROBE_GEMM_DX = 3,      /* bf16 dX GEMM main kernel                           */
   CG_PROBE_ATTN_FWD = 4,     /* attn_fwd_mfma                                      */
   CG_PROBE_ATTN_DQ = 5,      /* attn_bwd_dq_mfma                                   */
-  CG_PROBE_ATTN_DKDV = 6     /* attn_bwd_dkdv_mfma                                 */
+  CG_PROBE_ATTN_DKDV = 6,    /* attn_bwd_dkdv_mfma                                 */
+  CG_PROBE_GEMM_DW_GROUPED = 7 /* grouped weight-gradient GEMM (gemm_dw_kernel)      */
 };
 int cg_probe_enable(int kind);
 /* record 1 of every `every` launches of the probed kernel (default 1 = all); the launch
