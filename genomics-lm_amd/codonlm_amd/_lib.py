@@ -47,7 +47,7 @@ class GemmDesc(C.Structure):
                 ("drop_seed", u32), ("drop_p", f32), ("split_k", i32), ("workspace", vp)]
 
 
-DW_MAX = 16
+DW_MAX = 32
 
 
 class DwProduct(C.Structure):
@@ -139,6 +139,7 @@ SIGNATURES = {
     "cg_nonfinite_flag": (i32, [vp, i64, vp, vp]),
     "cg_model_param_layout": (i32, [C.POINTER(ModelCfg), C.POINTER(ParamEntry), i32, C.POINTER(i64)]),
     "cg_model_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
+    "cg_model_dw_plan": (i32, [C.POINTER(ModelCfg), C.POINTER(i32), C.POINTER(i32)]),
     "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
     "cg_model_aux_forward": (i32, [C.POINTER(Model), vp, i64, C.POINTER(vp), i64, vp]),
     "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),

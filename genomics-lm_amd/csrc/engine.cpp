@@ -25,7 +25,7 @@ enum { SITE_EMB = 0, SITE_ATTN = 1, SITE_MLP = 2 };
 
 struct Dims {
   int V, Vp, Tmax, L, H, KV, d, hd, kvd, Nqkv, hid, Hp, swiglu, rope;
-  int G;  // blocks per grouped weight-gradient launch (dw_plan)
+  int G, dw_bm;  // blocks per grouped weight-gradient launch and its tile rows (dw_plan)
 };
 
 bool dims_of(const cg_model_cfg* c, Dims& D) {
@@ -45,6 +45,7 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   D.hid = D.swiglu ? (int)(8 * (long long)c->n_embd / 3) : 4 * c->n_embd;
   D.Hp = D.swiglu ? (int)rup(D.hid, 64) : D.hid;
   D.G = 1;
+  D.dw_bm = 128;
   return true;
 }
 
@@ -58,26 +59,39 @@ int device_cus() {
   }
   return n;
 }
-// Blocks per grouped dW launch (bf16 engine).  A group's tiles run as one persistent launch with
-// one workgroup per CU and every tile costing about the same (full-token reduction), so the
-// launch takes ceil(tiles / CUs) rounds: pick the group size with the fewest rounds per block,
-// the smaller group on ties (its gradients are final -- and all-reduced -- earlier).
-// CG_DW_GROUP forces a size.
-int dw_plan(const cg_model_cfg* c, const Dims& D) {
-  if (c->dtype != CG_BF16 || D.L <= 0) return 1;
-  static const int forced = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
+// Group size and tile of the grouped dW launches (bf16 engine).  A group's tiles run as one
+// persistent launch with one workgroup per CU and every tile costing about the same (full-token
+// reduction), so a group takes ceil(tiles / CUs) rounds of its tile's cost.  Candidates: 128-row
+// tiles (4 waves, cost 1) and 256-row tiles (8 waves, cost 1.38 -- twice the work in 1.38x the
+// time, measured at K = 16384 on the C4/C5 shapes, tools/dw_grouped.py); the plan minimises the
+// summed cost of the groups (G, G, ..., remainder) and, on ties, prefers the smaller group (its
+// gradients are final -- and all-reduced -- earlier).  CG_DW_GROUP / CG_DW_BM force a choice.
+struct DwPlan {
+  int G, bm;
+};
+DwPlan dw_plan(const cg_model_cfg* c, const Dims& D) {
+  if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128};
+  static const int forced_g = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
+  static const int forced_bm = [] { const char* e = getenv("CG_DW_BM"); return e ? atoi(e) : 0; }();
   const int gmax = std::min(D.L, CG_DW_MAX / 4);
-  if (forced > 0) return std::min(forced, gmax);
-  const int d = D.d;
-  const int per_layer = cg_gemm_dw_tiles(0, D.Nqkv, d) + cg_gemm_dw_tiles(0, d, d) +
-                        (D.swiglu ? cg_gemm_dw_tiles(0, 2 * D.Hp, d) + cg_gemm_dw_tiles(0, d, D.Hp)
-                                  : cg_gemm_dw_tiles(0, D.hid, d) + cg_gemm_dw_tiles(0, d, D.hid));
-  const int cus = device_cus();
-  int best = 1;
+  const int d = D.d, cus = device_cus();
+  DwPlan best{1, 128};
   double best_cost = 1e30;
-  for (int g = 1; g <= gmax; ++g) {
-    const double cost = (double)((g * per_layer + cus - 1) / cus) / g;
-    if (cost < best_cost - 1e-9) best_cost = cost, best = g;
+  for (int bm : {128, 256}) {
+    if (forced_bm && bm != forced_bm) continue;
+    const double tile_cost = bm == 128 ? 1.0 : 1.38;
+    const int per_layer = cg_gemm_dw_tiles(bm, D.Nqkv, d) + cg_gemm_dw_tiles(bm, d, d) +
+                          (D.swiglu ? cg_gemm_dw_tiles(bm, 2 * D.Hp, d) + cg_gemm_dw_tiles(bm, d, D.Hp)
+                                    : cg_gemm_dw_tiles(bm, D.hid, d) + cg_gemm_dw_tiles(bm, d, D.hid));
+    for (int g = 1; g <= gmax; ++g) {
+      if (forced_g && g != std::min(forced_g, gmax)) continue;
+      double cost = 0;
+      for (int left = D.L; left > 0; left -= g) {
+        const int n = std::min(g, left);
+        cost += (double)((n * per_layer + cus - 1) / cus) * tile_cost;
+      }
+      if (cost < best_cost - 1e-9) best_cost = cost, best = {g, bm};
+    }
   }
   return best;
 }
@@ -299,7 +313,9 @@ struct Ctx {
 
 int make_ctx(const cg_model* m, int B, int T, void* stream, Ctx& C) {
   if (!dims_of(&m->cfg, C.D)) return CG_EINVAL;
-  C.D.G = dw_plan(&m->cfg, C.D);
+  const DwPlan pl = dw_plan(&m->cfg, C.D);
+  C.D.G = pl.G;
+  C.D.dw_bm = pl.bm;
   build_layout(&m->cfg, C.D, C.Lo);
   C.m = m;
   C.B = B; C.T = T; C.M = (long long)B * T;
@@ -459,6 +475,7 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
   cg_dw_group grp;
   memset(&grp, 0, sizeof(grp));
   grp.K = (int)C.M;
+  grp.tile_m = D.dw_bm;
   auto add = [&](const void* dy, int n_out, const void* x, int k_out, long long goff) -> int {
     if (C.dt != CG_BF16) return lin_dw(C, dy, n_out, x, k_out, n_out, k_out, goff, k_out, accumulate);
     cg_dw_product& q = grp.p[grp.n++];
@@ -590,10 +607,21 @@ extern "C" int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* ou
   return n;
 }
 
+extern "C" int cg_model_dw_plan(const cg_model_cfg* cfg, int* group_layers, int* tile_m) {
+  Dims D;
+  if (!dims_of(cfg, D)) return CG_EINVAL;
+  const DwPlan pl = dw_plan(cfg, D);
+  if (group_layers) *group_layers = pl.G;
+  if (tile_m) *tile_m = pl.bm;
+  return CG_OK;
+}
+
 extern "C" size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T) {
   Dims D;
   if (!dims_of(cfg, D)) return 0;
-  D.G = dw_plan(cfg, D);
+  const DwPlan pl = dw_plan(cfg, D);
+  D.G = pl.G;
+  D.dw_bm = pl.bm;
   Acts A;
   return carve(cfg, D, B, T, nullptr, A);
 }

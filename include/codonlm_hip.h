@@ -77,7 +77,7 @@ int cg_gemm_set_pers(int mode);
  * Each output tile is reduced over all K rows inside one workgroup (no split-K partials);
  * the tiles of all products form one persistent launch (tile_m = 128 or 256 rows of C per
  * tile, 0 = default; env CG_DW_BM).  K % 64 == 0; N_out, K_out, lda, ldb % 8 == 0; ldc % 4. */
-#define CG_DW_MAX 16
+#define CG_DW_MAX 32
 typedef struct {
   const void* A; long long lda;
   const void* B; long long ldb;
@@ -277,6 +277,9 @@ typedef struct {
 int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* out, int max,
                           long long* total_elems);
 size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T);
+/* the grouped weight-gradient plan of the bf16 engine: blocks per grouped dW launch and the
+ * tile rows (128 or 256) chosen for this configuration on the current device */
+int cg_model_dw_plan(const cg_model_cfg* cfg, int* group_layers, int* tile_m);
 
 typedef struct {
   cg_model_cfg cfg;
