@@ -114,10 +114,12 @@ SIGNATURES = {
     "cg_embed_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, u32, f32, i32, vp, vp]),
     "cg_segment_starts": (i32, [vp, vp, i32, i32, i32, vp]),
     "cg_rope_tab": (i32, [i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, i32, vp]),
-    "cg_attn_fwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp]),
+    "cg_attn_fwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp, vp]),
+    "cg_attn_drop_mask_bytes": (sz, [i32, i32, i32]),
+    "cg_attn_drop_mask": (i32, [i32, i32, i32, u32, f32, vp, vp]),
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
-                          u32, f32, vp, vp]),
+                          u32, f32, vp, vp, vp]),
     "cg_ce_workspace": (sz, [i32]),
     "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, vp]),
     "cg_swiglu_fwd": (i32, [i32, vp, i64, i32, vp, i64, i32, i32, vp]),

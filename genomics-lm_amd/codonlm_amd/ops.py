@@ -120,22 +120,31 @@ def segment_starts(idx, sep_id):
     return out
 
 
-def attn_fwd(qkv, segstart, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0):
+def attn_drop_mask(B, T, H, drop_seed, drop_p, device):
+    """Attention-dropout keep bits (query-major + key-major words) for cg_attn_fwd / cg_attn_bwd."""
+    n = int(L.lib.cg_attn_drop_mask_bytes(B, T, H))
+    mask = torch.empty(max(n, 4) // 4, dtype=torch.int32, device=device)
+    L.check(L.lib.cg_attn_drop_mask(B, T, H, int(drop_seed) & 0xFFFFFFFF, float(drop_p), mask.data_ptr(),
+                                    L.stream_ptr(device)), "cg_attn_drop_mask")
+    return mask
+
+
+def attn_fwd(qkv, segstart, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None):
     y = torch.empty(B * T, H * hd, dtype=qkv.dtype, device=qkv.device)
     lse = torch.empty(B * H * T, dtype=torch.float32, device=qkv.device)
     L.check(L.lib.cg_attn_fwd(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
                               lse.data_ptr(), B, T, H, KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF,
-                              float(drop_p), L.stream_ptr(qkv.device)), "cg_attn_fwd")
+                              float(drop_p), _p(drop_mask), L.stream_ptr(qkv.device)), "cg_attn_fwd")
     return y, lse
 
 
-def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0):
+def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None):
     dqkv = torch.zeros_like(qkv)
     ws = torch.empty(int(L.lib.cg_attn_bwd_workspace(B, T, H)) // 4 + 1, dtype=torch.float32, device=qkv.device)
     L.check(L.lib.cg_attn_bwd(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
                               dy.data_ptr(), dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), B, T, H,
-                              KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF, float(drop_p), ws.data_ptr(),
-                              L.stream_ptr(qkv.device)), "cg_attn_bwd")
+                              KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF, float(drop_p), _p(drop_mask),
+                              ws.data_ptr(), L.stream_ptr(qkv.device)), "cg_attn_bwd")
     return dqkv
 
 

@@ -265,9 +265,20 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_vec(const T* __restrict__ qk
 // ---------------------------------------------------------------------------
 // host entry points
 // ---------------------------------------------------------------------------
+extern "C" size_t cg_attn_drop_mask_bytes(int B, int T, int H) {
+  return B <= 0 || T <= 0 || H <= 0 ? 0 : attn_drop_mask_words(B, T, H) * sizeof(uint32_t);
+}
+
+extern "C" int cg_attn_drop_mask(int B, int T, int H, uint32_t drop_seed, float drop_p, void* mask, void* stream) {
+  if (!(drop_p > 0.f) || drop_p >= 1.f) return CG_EINVAL;
+  if (!mask) return CG_EINVAL;
+  if (B == 0 || T == 0) return CG_OK;
+  return attn_drop_mask_launch((uint32_t*)mask, B, T, H, drop_seed, cg_drop_threshold(drop_p), (hipStream_t)stream);
+}
+
 extern "C" int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, void* y,
                            long long ldy, float* lse, int B, int T, int H, int KV, int hd, int window,
-                           uint32_t drop_seed, float drop_p, void* stream) {
+                           uint32_t drop_seed, float drop_p, const void* drop_mask, void* stream) {
   if (KV <= 0 || H % KV) return CG_EINVAL;
   if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
   if (B == 0 || T == 0) return CG_OK;
@@ -277,7 +288,7 @@ extern "C" int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const in
   const float scale = 1.0f / sqrtf((float)hd);
   if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, ldy)) {
     return attn_fwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (bf16_t*)y, ldy, lse, B, T, H, KV, hd, window,
-                                drop_seed, thr, dscale, scale, s);
+                                drop_seed, thr, dscale, scale, (const uint32_t*)drop_mask, s);
   }
   dim3 g(cg_cdiv(T, AV_TQ), B * H);
   if (dtype == CG_BF16)
@@ -295,7 +306,7 @@ extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return (size_t)B 
 extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const void* y,
                            long long ldy, const void* dy, long long lddy, const float* lse, void* dqkv,
                            long long lddqkv, int B, int T, int H, int KV, int hd, int window, uint32_t drop_seed,
-                           float drop_p, void* ws, void* stream) {
+                           float drop_p, const void* drop_mask, void* ws, void* stream) {
   if (KV <= 0 || H % KV) return CG_EINVAL;
   if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
   if (B == 0 || T == 0) return CG_OK;
@@ -309,7 +320,7 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
     // delta = rowsum(dO o O) is computed inside the dQ kernel
     return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)y, ldy, (const bf16_t*)dy,
                                 lddy, lse, delta, (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr,
-                                dscale, scale, s);
+                                dscale, scale, (const uint32_t*)drop_mask, s);
   }
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const bf16_t*)y, ldy,

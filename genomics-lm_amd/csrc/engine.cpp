@@ -187,6 +187,9 @@ struct LayerAct {
   void *h1, *qkv, *y, *h2, *a, *g, *gu, *s;
   // bf16 mode: per-step transposed copies of the shadow weights (K-contiguous dX operands)
   void *qkvT, *pT, *w1T, *w2T, *wguT, *wdT;
+  // bf16 training with dropout: this block's attention keep bits (cg_attn_drop_mask), made by
+  // the forward and read again by the backward
+  void* dmask;
 };
 // per-block gradient operands kept until the block's grouped dW launch (slot = position of
 // the block inside its group): dY of fc2/down (gin), of fc1/gate|up (dmlp), of proj (gattn),
@@ -297,6 +300,10 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
       a.wdT = w.take<char>((size_t)D.Hp * d * 2);
     }
   }
+  static const bool mask_env = [] { const char* e = getenv("CG_ATTN_DROP_MASK"); return !e || atoi(e) != 0; }();
+  const bool dmask = mask_env && c->dtype == CG_BF16 && c->dropout > 0.f;
+  for (int l = 0; l < D.L; ++l)
+    A.la[l].dmask = dmask ? w.take<char>(cg_attn_drop_mask_bytes(B, T, D.H)) : nullptr;
   return w.off + 256;
 }
 
@@ -660,8 +667,10 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     g.epilogue = CG_EPI_BIAS; g.bias = P(C, o.bqkv);
     CK(cg_gemm(&g, C.s));
     if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
+    const void* dmask = p > 0.f ? a.dmask : nullptr;
+    if (dmask) CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
     CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
-                   window, site_seed(seed, l, SITE_ATTN), p, C.s));
+                   window, site_seed(seed, l, SITE_ATTN), p, dmask, C.s));
     g = lin_fwd(C, a.y, d, o.wp, d, d, d, a.xmid, d);
     g.c_dtype = CG_F32;
     g.epilogue = CG_EPI_BIAS | CG_EPI_RESID; g.bias = P(C, o.bp); g.resid = xl; g.ldr = d;
@@ -831,7 +840,8 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     cg_gemm_desc g = lin_dx(C, sl.gattn, d, o.wp, d, d, d, A.dsmall, d, a.pT);
     CK(cg_gemm(&g, C.s));
     CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, sl.dqkv,
-                   D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, A.delta, C.s));
+                   D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p,
+                   p > 0.f ? a.dmask : nullptr, A.delta, C.s));
     if (D.rope)
       CK(cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
     CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));

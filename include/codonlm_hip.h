@@ -140,13 +140,20 @@ int cg_rope_tab(int dtype, void* qkv, long long ldqkv, int B, int T, int H, int 
  * lse: [B*H*T] fp32 (natural-log logsumexp of the scaled scores). window<=0: none. */
 int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
                 void* y, long long ldy, float* lse, int B, int T, int H, int KV, int hd,
-                int window, uint32_t drop_seed, float drop_p, void* stream);
+                int window, uint32_t drop_seed, float drop_p, const void* drop_mask, void* stream);
+/* Attention-dropout keep bits (the same keep(seed, (b*H+h)*T + q, key) as the in-kernel hash),
+ * precomputed once per (layer, step) so the bf16 MFMA kernels test one bit per (query, key):
+ * a query-major bit array over the causal lower triangle, in a buffer of
+ * cg_attn_drop_mask_bytes(B, T, H) bytes.  drop_mask (fwd / bwd): such a buffer made with the
+ * same seed and p, or NULL to hash in the kernels (identical keep decisions). */
+size_t cg_attn_drop_mask_bytes(int B, int T, int H);
+int cg_attn_drop_mask(int B, int T, int H, uint32_t drop_seed, float drop_p, void* mask, void* stream);
 /* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: cg_attn_bwd_workspace() */
 size_t cg_attn_bwd_workspace(int B, int T, int H);
 int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
                 const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
                 void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
-                uint32_t drop_seed, float drop_p, void* ws, void* stream);
+                uint32_t drop_seed, float drop_p, const void* drop_mask, void* ws, void* stream);
 
 /* Label-smoothed, class-weighted, ignore_index cross-entropy fwd+bwd over logits rows
  * (F.cross_entropy at model_tiny_gpt.py:343-349).  logits fp32 [rows][ldl], V used

@@ -229,6 +229,55 @@ def test_attention_mfma_full_geometry(B, T, H, KV, hd, p):
         assert e <= 2e-2, (name, e)
 
 
+def _mask_bits(words, T):
+    """Unpack attn_drop_mask words [BH, T, wpr] (pair-split order) into bool [BH, T, T]."""
+    w = words.cpu().numpy().view(np.uint32)
+    i = np.arange(T)
+    bit = (i % 32 >> 1) + 16 * (i % 2)
+    return ((w[:, :, i // 32] >> bit.astype(np.uint32)) & 1).astype(bool)
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 200, 3), (1, 1024, 2), (1, 64, 1), (1, 129, 1)])
+def test_attn_drop_mask_bits(B, T, H):
+    """The precomputed attention keep bits equal the oracle's dropout_keep on every causal
+    (query, key) pair."""
+    ops = _ops()
+    seed, p = 4242, 0.1
+    mask = ops.attn_drop_mask(B, T, H, seed, p, DEV)
+    torch.cuda.synchronize()
+    wpr = 2 * ((T + 63) // 64)
+    assert mask.numel() == B * H * T * wpr
+    qm = _mask_bits(mask.view(B * H, T, wpr), T)        # [bh, q, key]
+    keep = O.dropout_keep(seed, np.arange(B * H * T)[:, None], np.arange(T)[None, :], p).reshape(B * H, T, T)
+    causal = np.tril(np.ones((T, T), dtype=bool))[None]
+    assert np.array_equal(qm & causal, keep & causal)
+    assert 0.85 < keep[causal.repeat(B * H, 0)].mean() < 0.95
+
+
+@pytest.mark.parametrize("B,T,H,KV,hd", [(2, 1024, 8, 8, 64), (2, 512, 8, 4, 48), (1, 200, 4, 2, 32),
+                                         (1, 129, 2, 1, 64)])
+def test_attention_drop_mask_path_matches_hash_path(B, T, H, KV, hd):
+    """bf16 MFMA attention with precomputed keep bits vs the in-kernel hash: identical keep
+    decisions, so the forward is bitwise equal; the backward differs only by fma contraction
+    (rel-L2 <= 1e-3)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(hd + T)
+    N = (H + 2 * KV) * hd
+    qkv = _bf(torch.randn(B * T, N, generator=g)).to(DEV, torch.bfloat16)
+    idx = torch.randint(4, 68, (B, T), generator=g)
+    idx[0, T // 3] = 3
+    seg = ops.segment_starts(idx.to(DEV), 3)
+    seed, p = 31337, 0.1
+    mask = ops.attn_drop_mask(B, T, H, seed, p, DEV)
+    y0, l0 = ops.attn_fwd(qkv, seg, B, T, H, KV, hd, drop_seed=seed, drop_p=p)
+    y1, l1 = ops.attn_fwd(qkv, seg, B, T, H, KV, hd, drop_seed=seed, drop_p=p, drop_mask=mask)
+    assert torch.equal(y0, y1) and torch.equal(l0, l1)
+    dy = _bf(torch.randn(B * T, H * hd, generator=g)).to(DEV, torch.bfloat16)
+    d0 = ops.attn_bwd(qkv, seg, y0, dy, l0, B, T, H, KV, hd, drop_seed=seed, drop_p=p).float()
+    d1 = ops.attn_bwd(qkv, seg, y0, dy, l0, B, T, H, KV, hd, drop_seed=seed, drop_p=p, drop_mask=mask).float()
+    assert float((d1 - d0).norm() / d0.norm()) <= 1e-3
+
+
 @pytest.mark.parametrize("eps,weighted", [(0.0, False), (0.05, False), (0.1, True)])
 def test_cross_entropy(eps, weighted):
     ops = _ops()

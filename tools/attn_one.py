@@ -1,4 +1,6 @@
-"""One forward + backward of the C4 attention (dropout 0.1, SEP segments), for PMC passes."""
+"""One forward + backward of the C4 attention (dropout 0.1, SEP segments), for PMC passes.
+Uses the engine's path: keep bits precomputed by cg_attn_drop_mask (ATTN_HASH=1: in-kernel hash)."""
+import os
 import sys
 from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "genomics-lm_amd"))
@@ -10,9 +12,11 @@ g = torch.Generator().manual_seed(0)
 qkv = (torch.randn(B * T, 3 * H * hd, generator=g) * 0.5).to("cuda", torch.bfloat16)
 idx = torch.randint(4, 68, (B, T), generator=g)
 seg = ops.segment_starts(idx.to("cuda"), 3)
+hashed = os.environ.get("ATTN_HASH") == "1"
 for _ in range(2):
-    y, lse = ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=5, drop_p=0.1)
+    mask = None if hashed else ops.attn_drop_mask(B, T, H, 5, 0.1, "cuda")
+    y, lse = ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask)
     dy = torch.randn_like(y)
-    ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, H, hd, drop_seed=5, drop_p=0.1)
+    ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask)
 torch.cuda.synchronize()
 print("ok")

@@ -61,7 +61,7 @@ lse = torch.empty(B * H * T, dtype=torch.float32, device=dev)
 
 def ours_fwd():
     L.check(L.lib.cg_attn_fwd(L.CG_BF16, qkv.data_ptr(), qkv.stride(0), None, y.data_ptr(), y.stride(0),
-                              lse.data_ptr(), B, T, H, H, hd, 0, 0, 0.0, L.stream_ptr(qkv.device)), "fwd")
+                              lse.data_ptr(), B, T, H, H, hd, 0, 0, 0.0, None, L.stream_ptr(qkv.device)), "fwd")
 
 
 def sdpa_fwd():
