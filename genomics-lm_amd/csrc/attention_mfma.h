@@ -20,6 +20,9 @@
 #ifndef ATTN_FWD_WPS
 #define ATTN_FWD_WPS 2
 #endif
+#ifndef ATTN_DQ_WPS
+#define ATTN_DQ_WPS 3  // waves per SIMD the dQ kernel is register-limited to (<= 168 VGPRs)
+#endif
 
 namespace fa {
 constexpr int HDP = 64;        // padded head dim held in LDS / registers
@@ -431,7 +434,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
 // dS^T = P^T o (dP^T - delta),  dQ^T[d][q] += K^T[d][key] dS^T[key][q]
 // ============================================================================
 template <int DROP, int HD>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, long long ld,
+__global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_t* __restrict__ qkv, long long ld,
                                                            const int32_t* __restrict__ seg,
                                                            const bf16_t* __restrict__ dy, long long lddy,
                                                            const bf16_t* __restrict__ yo, long long ldy,
@@ -504,9 +507,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
       if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * (t + 1));
     }
     const int k0 = t * KT;
-    // FULL (compile-time): every (query, key) of the wave's tile visible -- no per-element mask
-    auto body = [&](auto full_c) __attribute__((always_inline)) {
-      constexpr bool FULL = decltype(full_c)::value;
+    // full: every (query, key) of the wave's tile visible.  Otherwise the invisible scores are
+    // set to -inf before the exponent; the branch touches only s, so the dQ accumulators keep
+    // their registers across it (a branch around the whole body made hipcc copy them back at
+    // the join)
+    auto body = [&](bool full) __attribute__((always_inline)) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         v16f s = zero16(), dp = zero16();
@@ -518,17 +523,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
           }
         }
         const int kq = myq - k0 - kb * 32, kl = lo - k0 - kb * 32;
+        if (!full) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int j = acc_row(r, lane);
+            s[r] = ((j > kq) | (j < kl)) ? -INFINITY : s[r];
+          }
+        }
         const uint32_t hb = hrow + ((uint32_t)((k0 + kb * 32) >> 1) + 2u * (uint32_t)(lane >> 5)) * CG_COLK;
         const uint32_t wb = (kb ? wc.y : wc.x) >> (2 * (lane >> 5));
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const int j = acc_row(r, lane);
-          float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
-          float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c, -lse2));
-          if constexpr (!FULL) {  // bitwise |: no short-circuit branches
-            p0 = ((j > kq) | (j < kl)) ? 0.f : p0;
-            p1 = ((j + 1 > kq) | (j + 1 < kl)) ? 0.f : p1;
-          }
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c, -lse2));
           float d0 = dp[r], d1 = dp[r + 1];
           if constexpr (DROP == 1) {
             const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
@@ -554,10 +561,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_mfma(const bf16_t* __restr
         }
       }
     };
-    if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
-      if ((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max)) body(std::true_type{});
-      else body(std::false_type{});
-    }
+    if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) body((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max));
     dma_drain();
     __syncthreads();
   }
@@ -706,9 +710,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     // wave activity: some query q in [q0, q0+63] sees some key in [kw0, kw0+31]
     const int qlast = min(T - 1, q0 + KT - 1);
     const bool active = (qlast >= kw0) && (los[0] <= kw0 + 31);
-    // FULL (compile-time): every (query, key) of the wave's tile visible -- no per-element mask
-    auto body = [&](auto full_c) __attribute__((always_inline)) {
-      constexpr bool FULL = decltype(full_c)::value;
+    // full: every (query, key) of the wave's tile visible.  Otherwise the invisible scores are
+    // set to -inf before the exponent (the branch touches only s: the dK/dV accumulators keep
+    // their registers across it)
+    auto body = [&](bool full) __attribute__((always_inline)) {
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         v16f s = zero16(), dp = zero16();
@@ -719,16 +724,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Di, qb * 32, ks, lane), vf[ks], dp, 0, 0, 0);
           }
         }
+        if (!full) {
+#pragma unroll
+          for (int rg = 0; rg < 16; rg += 4) {
+            const int qi = qb * 32 + acc_row(rg, lane);
+            const int4 lo4 = *(const int4*)(los + qi);
+            const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int q = q0 + qi + u;
+              s[rg + u] = ((mykey > q) | (mykey < lov[u]) | (q >= T)) ? -INFINITY : s[rg + u];
+            }
+          }
+        }
         v16f pd;
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 4) {
           const int qi = qb * 32 + acc_row(rg, lane);  // 4 consecutive queries qi..qi+3
           const float4 l4 = *(const float4*)(lse2s + qi);
           const float4 d4 = *(const float4*)(dls + qi);
-          const int4 lo4 = *(const int4*)(los + qi);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
           const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
-          const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
           uint4 hr4 = make_uint4(0, 0, 0, 0);
           if constexpr (DROP == 1) hr4 = *(const uint4*)(hrs + qi);
           uint4 mw4 = make_uint4(0, 0, 0, 0);
@@ -738,9 +754,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int r = rg + u;
-            const int q = q0 + qi + u;
-            float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[u]));
-            if constexpr (!FULL) p = ((mykey > q) | (mykey < lov[u]) | (q >= T)) ? 0.f : p;
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[u]));
             float d = dp[r];
             float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
             if constexpr (DROP == 1) {
@@ -774,10 +788,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         }
       }
     };
-    if (active) {
-      if ((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (los[qlast - q0] <= kw0)) body(std::true_type{});
-      else body(std::false_type{});
-    }
+    if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (los[qlast - q0] <= kw0));
     if (more) stage_store(nx, smem + ((it & 1) ^ 1) * BUF);
     cur = nx;
     dma_drain();
