@@ -59,39 +59,54 @@ int device_cus() {
   }
   return n;
 }
-// Group size and tile of the grouped dW launches (bf16 engine).  A group's tiles run as one
+// Group size and tiles of the grouped dW launches (bf16 engine).  A group's tiles run as one
 // persistent launch with one workgroup per CU and every tile costing about the same (full-token
-// reduction), so a group takes ceil(tiles / CUs) rounds of its tile's cost.  Candidates: 128-row
-// tiles (4 waves, cost 1) and 256-row tiles (8 waves, cost 1.38 -- twice the work in 1.38x the
-// time, measured at K = 16384 on the C4/C5 shapes, tools/dw_grouped.py); the plan minimises the
+// reduction), so a group takes ceil(tiles / CUs) rounds of its tile's cost.  Tile candidates
+// (cg_gemm_dw_tiles codes): 128 x 128 (cost 1), 256 x 128 (1.38: twice the work in 1.38x the
+// time) and 256 x 256 (2.35: 4x the work; a 2-stage ring, its DMA latency partly exposed),
+// measured at K = 16384 on the C4/C5 shapes (tools/dw_grouped.py).  Each group takes its
+// cheapest tile (a short remainder group often prefers the smaller tile); the plan minimises the
 // summed cost of the groups (G, G, ..., remainder) and, on ties, prefers the smaller group (its
 // gradients are final -- and all-reduced -- earlier).  CG_DW_GROUP / CG_DW_BM force a choice.
 struct DwPlan {
-  int G, bm;
+  int G, bm;  // group size, tile of a full group
 };
-DwPlan dw_plan(const cg_model_cfg* c, const Dims& D) {
-  if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128};
-  static const int forced_g = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
-  static const int forced_bm = [] { const char* e = getenv("CG_DW_BM"); return e ? atoi(e) : 0; }();
-  const int gmax = std::min(D.L, CG_DW_MAX / 4);
+static int dw_forced_bm() {
+  static const int forced = [] { const char* e = getenv("CG_DW_BM"); return e ? atoi(e) : 0; }();
+  return forced;
+}
+// cheapest tile for a group of n blocks, and its cost
+static int dw_tile_for(const Dims& D, int n, double* cost_out) {
   const int d = D.d, cus = device_cus();
-  DwPlan best{1, 128};
+  int best = 256;
   double best_cost = 1e30;
-  for (int bm : {128, 256}) {
-    if (forced_bm && bm != forced_bm) continue;
-    const double tile_cost = bm == 128 ? 1.0 : 1.38;
+  for (int bm : {128, 256, 512}) {
+    if (dw_forced_bm() && bm != dw_forced_bm()) continue;
+    const double tile_cost = bm == 128 ? 1.0 : bm == 256 ? 1.38 : 2.35;
     const int per_layer = cg_gemm_dw_tiles(bm, D.Nqkv, d) + cg_gemm_dw_tiles(bm, d, d) +
                           (D.swiglu ? cg_gemm_dw_tiles(bm, 2 * D.Hp, d) + cg_gemm_dw_tiles(bm, d, D.Hp)
                                     : cg_gemm_dw_tiles(bm, D.hid, d) + cg_gemm_dw_tiles(bm, d, D.hid));
-    for (int g = 1; g <= gmax; ++g) {
-      if (forced_g && g != std::min(forced_g, gmax)) continue;
-      double cost = 0;
-      for (int left = D.L; left > 0; left -= g) {
-        const int n = std::min(g, left);
-        cost += (double)((n * per_layer + cus - 1) / cus) * tile_cost;
-      }
-      if (cost < best_cost - 1e-9) best_cost = cost, best = {g, bm};
+    const double cost = (double)((n * per_layer + cus - 1) / cus) * tile_cost;
+    if (cost < best_cost - 1e-9) best_cost = cost, best = bm;
+  }
+  if (cost_out) *cost_out = best_cost;
+  return best;
+}
+DwPlan dw_plan(const cg_model_cfg* c, const Dims& D) {
+  if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128};
+  static const int forced_g = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
+  const int gmax = std::min(D.L, CG_DW_MAX / 4);
+  DwPlan best{1, 128};
+  double best_cost = 1e30;
+  for (int g = 1; g <= gmax; ++g) {
+    if (forced_g && g != std::min(forced_g, gmax)) continue;
+    double cost = 0;
+    for (int left = D.L; left > 0; left -= g) {
+      double cg;
+      dw_tile_for(D, std::min(g, left), &cg);
+      cost += cg;
     }
+    if (cost < best_cost - 1e-9) best_cost = cost, best = {g, dw_tile_for(D, g, nullptr)};
   }
   return best;
 }
@@ -482,7 +497,7 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
   cg_dw_group grp;
   memset(&grp, 0, sizeof(grp));
   grp.K = (int)C.M;
-  grp.tile_m = D.dw_bm;
+  grp.tile_m = l_hi - l_lo + 1 == D.G ? D.dw_bm : dw_tile_for(D, l_hi - l_lo + 1, nullptr);
   auto add = [&](const void* dy, int n_out, const void* x, int k_out, long long goff) -> int {
     if (C.dt != CG_BF16) return lin_dw(C, dy, n_out, x, k_out, n_out, k_out, goff, k_out, accumulate);
     cg_dw_product& q = grp.p[grp.n++];

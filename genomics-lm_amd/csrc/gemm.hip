@@ -697,33 +697,37 @@ static int g_dw_bm = [] {
   const char* e = getenv("CG_DW_BM");
   return e ? atoi(e) : 128;
 }();
+static bool dw_tile_code(int bm) { return bm == 128 || bm == 129 || bm == 256 || bm == 512; }
 extern "C" int cg_gemm_dw_set_tile(int bm) {
   const int old = g_dw_bm;
-  if (bm == 128 || bm == 129 || bm == 256) g_dw_bm = bm;
+  if (dw_tile_code(bm)) g_dw_bm = bm;
   return old;
 }
+// tile codes: 128 / 129 = 128 x 128 (4 / 5 ring stages), 256 = 256 x 128 (3 stages),
+// 512 = 256 x 256 (2 stages of 64 KiB)
 extern "C" int cg_gemm_dw_tiles(int bm, int N_out, int K_out) {
-  if (bm != 128 && bm != 129 && bm != 256) bm = g_dw_bm;
-  return cg_cdiv(N_out, bm == 256 ? 256 : 128) * cg_cdiv(K_out, bfd::BN);
+  if (!dw_tile_code(bm)) bm = g_dw_bm;
+  return cg_cdiv(N_out, bm >= 256 ? 256 : 128) * cg_cdiv(K_out, bm == 512 ? 256 : 128);
 }
-template <int BM, int NS>
+template <int BM, int NS, int BNT = bfd::BN>
 static int launch_dw(bfd::Params& P, hipStream_t s) {
-  using G = bfd::Geo<BM, NS>;
+  using G = bfd::Geo<BM, NS, BNT>;
   int ntiles = 0;
   for (int i = 0; i < P.nprod; ++i) {
     bfd::Prod& pr = P.p[i];
-    pr.tiles_n = cg_cdiv(pr.K_out, bfd::BN);
+    pr.tiles_n = cg_cdiv(pr.K_out, BNT);
     pr.tile0 = ntiles;
     ntiles += cg_cdiv(pr.N_out, BM) * pr.tiles_n;
   }
   P.ntiles = ntiles;
   if (!ntiles) return CG_OK;
   const int grid = std::min(ntiles, cu_count());
-  (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS>, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+  (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            G::SMEM);
   double flops = 0;
   for (int i = 0; i < P.nprod; ++i) flops += 2.0 * P.p[i].N_out * (double)P.p[i].K_out * P.K;
   cg_probe_begin(CG_PROBE_GEMM_DW_GROUPED, s);
-  hipLaunchKernelGGL((gemm_dw_kernel<BM, NS>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
+  hipLaunchKernelGGL((gemm_dw_kernel<BM, NS, BNT>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
   cg_probe_end(CG_PROBE_GEMM_DW_GROUPED, s, flops);
   CG_LAUNCH_CHECK();
   return CG_OK;
@@ -756,6 +760,7 @@ extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
   const int bm = grp->tile_m > 0 ? grp->tile_m : g_dw_bm;
   // tile_m codes: 128 / 256 = rows of the C tile (ring of 4 / 3 stages); 129 / 257 = the same
   // tile with one more ring stage (5 / 4... 160 KB LDS for 128)
+  if (bm == 512) return launch_dw<256, 2, 256>(P, s);
   if (bm == 256) return launch_dw<256, 3>(P, s);
   if (bm == 129) return launch_dw<128, 5>(P, s);
   return launch_dw<128, 4>(P, s);

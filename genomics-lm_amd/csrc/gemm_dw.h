@@ -39,16 +39,18 @@ __device__ __forceinline__ void dma16_asm(__amdgpu_buffer_rsrc_t r, uint32_t lds
       : "memory");
 }
 
-template <int BM, int NSTAGE>
+// BNT: output-tile columns (128: waves of 64x64; 256: waves of 64x128, 8 B fragments per k-half)
+template <int BM, int NSTAGE, int BNT = BN>
 struct Geo {
-  static constexpr int WAVES = BM / 32;                   // (BM/64) x 2 waves of 64x64
+  static constexpr int WAVES = BM / 32;                   // (BM/64) x 2 waves of 64 x BNT/2
+  static constexpr int JN = BNT / 32;                     // 16-column blocks per wave
   static constexpr int THREADS = WAVES * 64;
   static constexpr int STAGES = NSTAGE;
   static constexpr int A_BYTES = BM * BKT * 2;
-  static constexpr int B_BYTES = BN * BKT * 2;
+  static constexpr int B_BYTES = BNT * BKT * 2;
   static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
   static constexpr int A_CHUNKS = A_BYTES / 1024 / WAVES;  // 4
-  static constexpr int B_CHUNKS = B_BYTES / 1024 / WAVES;  // 4 (BM 128) or 2 (BM 256)
+  static constexpr int B_CHUNKS = B_BYTES / 1024 / WAVES;  // 4 (BM 128), 2 (BM 256) or 4 (256 x 256)
   static constexpr int DPS = A_CHUNKS + B_CHUNKS;          // DMA wave-instructions per stage
   static constexpr int SMEM = STAGES * STAGE_BYTES;
 };
@@ -68,10 +70,11 @@ struct Params {
 };
 }  // namespace bfd
 
-template <int BM, int NSTAGE>
-__global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_kernel(const bfd::Params P) {
+template <int BM, int NSTAGE, int BNT>
+__global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_dw_kernel(const bfd::Params P) {
   using namespace bfd;
-  using G = Geo<BM, NSTAGE>;
+  using G = Geo<BM, NSTAGE, BNT>;
+  constexpr int JN = G::JN;
   constexpr int S = G::STAGES;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -81,7 +84,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_ke
   const int lb = cg_xcd_remap(blockIdx.x, nblk);  // an XCD's workgroups take consecutive tiles
   const int my_tiles = lb < P.ntiles ? (P.ntiles - 1 - lb) / nblk + 1 : 0;
   const int nt = P.K / BKT;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * (BNT / 2);
   if (my_tiles == 0) return;
 
   auto find = [&](int tile, int& pi) {
@@ -105,7 +108,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_ke
     find(tile, pi);
     const Prod& pr = P.p[pi];
     const int lt = tile - pr.tile0;
-    const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BN;
+    const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BNT;
     ra = __builtin_amdgcn_make_buffer_rsrc((void*)pr.A, (short)0,
                                            (int)(((long long)(P.K - 1) * pr.lda + pr.N_out) * 2), 0x00020000);
     rb = __builtin_amdgcn_make_buffer_rsrc((void*)pr.B, (short)0,
@@ -136,45 +139,73 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_ke
     advance();
   };
 
-  v4f acc[4][4];
+  v4f acc[4][JN];
   auto step = [&](int g) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * G::DPS) : "memory");
     __builtin_amdgcn_s_barrier();
     const char* st = smem + (g % S) * G::STAGE_BYTES;
     const char* as = st + (wm >> 7) * 16384;
     const int ar = wm & 127;
-    const char* bs = st + G::A_BYTES;
-    v8bf af[2][4], bfr[2][4];
+    const char* bs = st + G::A_BYTES + (wn >> 7) * 16384;  // the wave's 128-column sub-image
+    const int bc = wn & 127;
+    v8bf af[2][4], bfr[2][JN];
 #pragma unroll
     for (int i = 0; i < 4; ++i) af[0][i] = bfg::frag<false>(as, ar + 16 * i, 0, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[0][j] = bfg::frag<false>(bs, wn + 16 * j, 0, lane);
+    for (int j = 0; j < JN; ++j) bfr[0][j] = bfg::frag<false>(bs, bc + 16 * j, 0, lane);
     // the DMAs of stage g + S - 1 go into the slot step g - 1 read (every wave is past it)
     const uint32_t nx = lds0 + ((g + S - 1) % S) * G::STAGE_BYTES + wave * 1024;
     const uint32_t ao = a_org + dt * a_step, bo = b_org + dt * b_step;
+    if constexpr (JN == 4) {
 #pragma unroll
-    for (int gr = 0; gr < 8; ++gr) {
-      const int i = gr >> 1, j0 = 2 * (gr & 1);
-      acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0], af[0][i], acc[i][j0], 0, 0, 0);
-      acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
-      if (gr < 4) af[1][gr] = bfg::frag<false>(as, ar + 16 * gr, 1, lane);
-      else bfr[1][gr - 4] = bfg::frag<false>(bs, wn + 16 * (gr - 4), 1, lane);
-      if (gr < G::A_CHUNKS) dma16_asm(ra, nx + G::WAVES * gr * 1024, ao + va[gr]);
-      else if (gr < G::DPS) dma16_asm(rb, nx + G::A_BYTES + G::WAVES * (gr - G::A_CHUNKS) * 1024, bo + vb[gr - G::A_CHUNKS]);
+      for (int gr = 0; gr < 8; ++gr) {
+        const int i = gr >> 1, j0 = 2 * (gr & 1);
+        acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0], af[0][i], acc[i][j0], 0, 0, 0);
+        acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
+        if (gr < 4) af[1][gr] = bfg::frag<false>(as, ar + 16 * gr, 1, lane);
+        else bfr[1][gr - 4] = bfg::frag<false>(bs, bc + 16 * (gr - 4), 1, lane);
+        if (gr < G::A_CHUNKS) dma16_asm(ra, nx + G::WAVES * gr * 1024, ao + va[gr]);
+        else if (gr < G::DPS) dma16_asm(rb, nx + G::A_BYTES + G::WAVES * (gr - G::A_CHUNKS) * 1024, bo + vb[gr - G::A_CHUNKS]);
+      }
+    } else {
+      // 64 x 128 per wave: column block j's four MFMAs, then its half-1 fragment into the
+      // registers half 0's fragment j just released (and one of A's half-1 fragments, and a DMA)
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j], af[0][i], acc[i][j], 0, 0, 0);
+        bfr[1][j] = bfg::frag<false>(bs, bc + 16 * j, 1, lane);
+        if (j < 4) af[1][j] = bfg::frag<false>(as, ar + 16 * j, 1, lane);
+        if (j < G::A_CHUNKS) dma16_asm(ra, nx + G::WAVES * j * 1024, ao + va[j]);
+        else if (j < G::DPS) dma16_asm(rb, nx + G::A_BYTES + G::WAVES * (j - G::A_CHUNKS) * 1024, bo + vb[j - G::A_CHUNKS]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < JN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // half 0's fragment reads (2 tr-reads each)
+    if constexpr (JN == 4) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // half 0's fragment reads (2 tr-reads each)
 #pragma unroll
-    for (int gr = 0; gr < 8; ++gr) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-      if (gr < G::DPS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+      for (int gr = 0; gr < 8; ++gr) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        if (gr < G::DPS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    } else {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2 * (4 + JN), 0);
+#pragma unroll
+      for (int j = 0; j < JN; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        if (j < 4) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);  // B and A half-1 fragments
+        else __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        if (j < G::DPS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * JN, 0);
     }
-    __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
     advance();
   };
 
@@ -184,13 +215,13 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_ke
     find(tile, pi);
     const Prod& pr = P.p[pi];
     const int lt = tile - pr.tile0;
-    const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BN;
+    const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BNT;
     const int g4 = lane >> 4, r16 = lane & 15;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm + 16 * i + r16;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < JN; ++j) {
         const int n = n0 + wn + 16 * j + 4 * g4;
         if (m < pr.N_out && n < pr.K_out) {
           float4* c = (float4*)(pr.C + (long long)m * pr.ldc + n);
@@ -214,7 +245,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE>::THREADS), 1) void gemm_dw_ke
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < JN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
     for (int t = 0; t < nt; ++t, ++g) step(g);
     epilogue(k);
   }

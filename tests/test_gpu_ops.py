@@ -229,6 +229,33 @@ def test_attention_mfma_full_geometry(B, T, H, KV, hd, p):
         assert e <= 2e-2, (name, e)
 
 
+@pytest.mark.parametrize("tile", [128, 129, 256, 512])
+def test_gemm_dw_grouped_tiles(tile):
+    """Grouped full-reduction dW (cg_gemm_dw_grouped) for every tile code, against fp32 products
+    of the same bf16 operands: ragged N_out / K_out (partial tiles), strided operands, alpha and
+    accumulate, products of different shapes in one launch.  Bound: fp32 accumulation of exact
+    bf16 products over K = 2048 rows -> max error <= 1e-5 of the output scale."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(tile)
+    K = 2048
+    shapes = [(200, 136), (512, 384), (72, 520), (1536, 512)]
+    prods, refs = [], []
+    for i, (n, k) in enumerate(shapes):
+        dy_full = _bf(torch.randn(K, n + 8, generator=g)).to(DEV, torch.bfloat16)
+        dy = dy_full[:, :n]  # row stride n + 8
+        x = _bf(torch.randn(K, k, generator=g)).to(DEV, torch.bfloat16)
+        alpha, acc = (0.5, True) if i % 2 else (1.0, False)
+        out = torch.randn(n, k, generator=g).to(DEV) if acc else torch.empty(n, k, device=DEV)
+        ref = alpha * (dy.float().t() @ x.float()) + (out.clone() if acc else 0)
+        prods.append((dy, x, out, alpha, acc))
+        refs.append(ref)
+    ops.gemm_dw_grouped(prods, tile_m=tile)
+    torch.cuda.synchronize()
+    for (dy, x, out, _, _), ref in zip(prods, refs):
+        err = ((out - ref).abs().max() / ref.abs().max()).item()
+        assert err <= 1e-5, (tile, tuple(out.shape), err)
+
+
 def _mask_bits(words, T):
     """Unpack attn_drop_mask words [BH, T, wpr] (pair-split order) into bool [BH, T, T]."""
     w = words.cpu().numpy().view(np.uint32)

@@ -36,7 +36,7 @@ def timeit(fn, reps=10):
 for name, (M, d, nqkv, hid) in {"c4": (16384, 512, 1536, 2048), "c5": (16384, 384, 1152, 1536)}.items():
     prods = layer_products(M, d, nqkv, hid)
     # correctness (one product of each shape, both tiles)
-    for bm in (128, 256):
+    for bm in (128, 256, 512):
         ops.gemm_dw_grouped(prods, tile_m=bm)
         torch.cuda.synchronize()
         for dy, x, out, _, _ in prods:
@@ -44,17 +44,17 @@ for name, (M, d, nqkv, hid) in {"c4": (16384, 512, 1536, 2048), "c5": (16384, 38
             err = ((out - ref).abs().max() / ref.abs().max()).item()
             assert err < 1e-4, (name, bm, tuple(out.shape), err)
     flops = sum(2.0 * M * p[0].shape[1] * p[1].shape[1] for p in prods)
-    for bm in (128, 129, 256):
+    for bm in (128, 129, 256, 512):
         t1 = timeit(lambda: ops.gemm_dw_grouped(prods, tile_m=bm))
         print(f"{name} layer group  BM={bm}: {t1:8.1f} us  {flops / t1 / 1e6:7.1f} TF/s")
         for p in prods[:1]:
             f = 2.0 * M * p[0].shape[1] * p[1].shape[1]
             t = timeit(lambda: ops.gemm_dw_grouped([p], tile_m=bm))
             print(f"   single {tuple(p[2].shape)} BM={bm}: {t:8.1f} us  {f / t / 1e6:7.1f} TF/s")
-    for G in (2, 4):
+    for G in (2, 4, 5):
         many = prods * G  # same operands G times (L2/MALL-warm upper bound for a G-layer group)
         outs = [(a, b, torch.empty_like(c), al, ac) for a, b, c, al, ac in many]
-        for bm in (128, 129, 256):
+        for bm in (256, 512):
             t = timeit(lambda: ops.gemm_dw_grouped(outs, tile_m=bm))
             print(f"{name} {G}-layer group BM={bm}: {t:8.1f} us  {G * flops / t / 1e6:7.1f} TF/s  ({t / G:.1f} us/layer)")
     # the split-K path this replaces (dW = dY^T X via cg_gemm with MN-contiguous operands)
