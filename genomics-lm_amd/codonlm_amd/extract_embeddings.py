@@ -12,9 +12,10 @@ forward per batch on the GPU, and the pooling reads the engine's hidden-state bu
 place (cg_pool_hidden) -- no (B, T, d) copies leave HBM.  ``--dtype bf16`` selects the
 throughput engine; the default fp32 is the reference's arithmetic.
 
-Not supported (outside the hot path): shape-guided checkpoints, frozen dataset manifests
-(``--manifest``); a checkpoint that declares a manifest-bound dataset is refused like the
-reference does without a manifest.
+``--manifest`` binds a frozen dataset manifest exactly as the reference (:227-230, the
+``provenance`` module): the manifest is validated, and a corrected checkpoint must name the same
+dataset and vocabulary; without it such a checkpoint is refused.  Not supported (outside the hot
+path): shape-guided checkpoints.
 """
 from __future__ import annotations
 
@@ -31,6 +32,7 @@ import torch
 
 from . import ops
 from .checkpoints import build_codon_model_from_cfg, build_model_from_state, load_codon_checkpoint
+from .provenance import bind_checkpoint_dataset, bind_dataset_manifest
 
 POOLING_MODES = ("mean_nonpad", "mean_content", "eos")
 
@@ -151,7 +153,7 @@ def main(argv=None) -> None:
     ap.add_argument("--csv")
     ap.add_argument("--seq_col", default="seq")
     ap.add_argument("--mode", choices=["dna_cds", "codon_tokens"], default="dna_cds")
-    ap.add_argument("--manifest", type=Path, help="frozen dataset manifest (not supported on this path)")
+    ap.add_argument("--manifest", type=Path, help="frozen dataset manifest (corrected checkpoints)")
     ap.add_argument("--batch-size", type=int, default=16)
     ap.add_argument("--random-init-seed", type=int)
     ap.add_argument("--hidden-layers", default="final")
@@ -161,8 +163,6 @@ def main(argv=None) -> None:
     args = ap.parse_args(argv)
     if args.batch_size < 1:
         ap.error("--batch-size must be at least 1")
-    if args.manifest is not None:
-        raise NotImplementedError("--manifest (dataset provenance binding) is outside the MI355X hot path")
     layer_values = ["final" if v.strip() == "final" else int(v) for v in args.hidden_layers.split(",")]
     pooling_modes = [v.strip() for v in args.pooling_modes.split(",")]
 
@@ -176,10 +176,10 @@ def main(argv=None) -> None:
         ap.error(f"--hidden-layers must be drawn from {sorted(map(str, valid_layers))}")
     if not pooling_modes or any(m not in POOLING_MODES for m in pooling_modes):
         ap.error(f"--pooling-modes must be drawn from {sorted(POOLING_MODES)}")
-    manifest = cfg.get("dataset_manifest")
-    if isinstance(manifest, dict) and manifest.get("dataset_id") is not None:
-        raise RuntimeError("corrected checkpoint requires an explicit frozen dataset manifest")
-    checkpoint_dataset = {"status": "legacy_checkpoint_unverified", "dataset_id": None}
+    manifest_provenance = None
+    if args.manifest is not None:
+        _, manifest_provenance = bind_dataset_manifest(args.manifest)
+    checkpoint_dataset = bind_checkpoint_dataset(cfg, manifest_provenance)
     validate_vocabulary(itos, state_dict, cfg, itos_path)
     device = torch.device("cuda", torch.cuda.current_device())
     if args.random_init_seed is None:
@@ -238,7 +238,8 @@ def main(argv=None) -> None:
         "created_at": datetime.now(timezone.utc).isoformat(),
         "checkpoint": {"path": str(Path(checkpoint_path).resolve()), "sha256": _sha256(checkpoint_path)},
         "model_weights": {"sha256": weights_sha, "initialization": model_initialization},
-        "dataset_manifest": {"status": "legacy_unverified"}, "checkpoint_dataset": checkpoint_dataset,
+        "dataset_manifest": manifest_provenance or {"status": "legacy_unverified"},
+        "checkpoint_dataset": checkpoint_dataset,
         "vocabulary": {"path": str(itos_path.resolve()), "size": len(itos), "sha256": _sha256(itos_path)},
         "inputs": [{"path": str(p.resolve()), "sha256": _sha256(p)} for p in inputs],
         "mask_mode": "canonical_causal_segment" if model.sep_id is not None else "canonical_causal",
