@@ -119,7 +119,7 @@ SIGNATURES = {
     "cg_attn_drop_mask": (i32, [i32, i32, i32, u32, f32, vp, vp]),
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
-                          u32, f32, vp, vp, vp]),
+                          u32, f32, vp, vp, i64, vp, vp]),
     "cg_ce_workspace": (sz, [i32]),
     "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, vp]),
     "cg_swiglu_fwd": (i32, [i32, vp, i64, i32, vp, i64, i32, i32, vp]),

@@ -138,12 +138,16 @@ def attn_fwd(qkv, segstart, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, 
     return y, lse
 
 
-def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None):
+def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None,
+             bias_part=None):
+    """dqkv; with bias_part (fp32 [B*ceil(T/128)][ld >= (H+2KV) hd], bf16 MFMA path) also the per-tile
+    column sums of dqkv that cg_colsum_reduce turns into the q/k/v bias gradients."""
     dqkv = torch.zeros_like(qkv)
     ws = torch.empty(int(L.lib.cg_attn_bwd_workspace(B, T, H)) // 4 + 1, dtype=torch.float32, device=qkv.device)
     L.check(L.lib.cg_attn_bwd(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
                               dy.data_ptr(), dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), B, T, H,
                               KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF, float(drop_p), _p(drop_mask),
+                              _p(bias_part), 0 if bias_part is None else bias_part.stride(0),
                               ws.data_ptr(), L.stream_ptr(qkv.device)), "cg_attn_bwd")
     return dqkv
 

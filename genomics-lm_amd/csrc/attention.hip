@@ -306,7 +306,8 @@ extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return (size_t)B 
 extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const void* y,
                            long long ldy, const void* dy, long long lddy, const float* lse, void* dqkv,
                            long long lddqkv, int B, int T, int H, int KV, int hd, int window, uint32_t drop_seed,
-                           float drop_p, const void* drop_mask, void* ws, void* stream) {
+                           float drop_p, const void* drop_mask, float* bias_part, long long ld_part, void* ws,
+                           void* stream) {
   if (KV <= 0 || H % KV) return CG_EINVAL;
   if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
   if (B == 0 || T == 0) return CG_OK;
@@ -316,11 +317,13 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
   const float scale = 1.0f / sqrtf((float)hd);
   float* delta = (float*)ws;
   const long long nbt = (long long)B * H * T;
-  if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, lddy) && (lddqkv & 7) == 0 && (ldy & 7) == 0) {
+  const bool mfma = dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, lddy) && (lddqkv & 7) == 0 && (ldy & 7) == 0;
+  if (bias_part && (!mfma || ld_part < (long long)(H + 2 * KV) * hd)) return CG_EUNSUPPORTED;
+  if (mfma) {
     // delta = rowsum(dO o O) is computed inside the dQ kernel
     return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)y, ldy, (const bf16_t*)dy,
                                 lddy, lse, delta, (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr,
-                                dscale, scale, (const uint32_t*)drop_mask, s);
+                                dscale, scale, (const uint32_t*)drop_mask, bias_part, ld_part, s);
   }
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const bf16_t*)y, ldy,

@@ -176,6 +176,30 @@ __device__ __forceinline__ v16f zero16() {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// sum over the 32 lanes of a half-wave (lanes l and l^32 are summed separately)
+__device__ __forceinline__ float half_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  return v;
+}
+// The workgroup's 128 rows of two accumulator blocks x0 (columns 0..31) and x1 (32..63), one
+// row per lane-half, summed per column into red[wave][c0 + column] (LDS, 4 waves x stride)
+__device__ __forceinline__ void colsum_acc(const v16f& x0, const v16f& x1, float s, bool ok, float* red, int stride,
+                                           int c0, int wave, int lane) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float v0 = half_sum(ok ? x0[r] * s : 0.f);
+    const float v1 = half_sum(ok ? x1[r] * s : 0.f);
+    if ((lane & 31) == 0) {
+      red[wave * stride + c0 + acc_row(r, lane)] = v0;
+      red[wave * stride + c0 + 32 + acc_row(r, lane)] = v1;
+    }
+  }
+}
+
 // visible-key lower bound for query q (monotone non-decreasing in q)
 __device__ __forceinline__ int lo_of(const int32_t* seg, long long rowbase, int q, int T, int window) {
   if (q >= T) q = T - 1;
@@ -442,7 +466,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
                                                            float* __restrict__ delta, bf16_t* __restrict__ dqkv,
                                                            long long lddq, int T, int H, int KV, int hd_rt, int window,
                                                            uint32_t seed, uint32_t thr, float dscale, float scale,
-                                                           const uint32_t* __restrict__ qmask, int wpr) {
+                                                           const uint32_t* __restrict__ qmask, int wpr,
+                                                           float* __restrict__ bpart, long long ldp) {
   using namespace fa;
   constexpr int hd = HD;
   (void)hd_rt;
@@ -584,6 +609,14 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
       }
     }
   }
+  if (bpart) {  // q-bias gradient partial: column sums of this workgroup's dQ rows (fp32)
+    float* red = (float*)smem;  // the ring is idle after the last barrier
+    colsum_acc(a0, a1, scale, qok, red, 64, 0, wave, lane);
+    __syncthreads();
+    if (tid < hd)
+      bpart[((long long)b * gridDim.y + qtile) * ldp + (long long)hh * hd + tid] =
+          (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+  }
 }
 
 // ============================================================================
@@ -601,7 +634,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
                                                              bf16_t* __restrict__ dqkv, long long lddq, int T, int H,
                                                              int KV, int hd_rt, int window, uint32_t seed, uint32_t thr,
                                                              float dscale, float scale,
-                                                             const uint32_t* __restrict__ qmask, int wpr) {
+                                                             const uint32_t* __restrict__ qmask, int wpr,
+                                                             float* __restrict__ bpart, long long ldp) {
   using namespace fa;
   constexpr int hd = HD;
   (void)hd_rt;
@@ -821,6 +855,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       }
     }
   }
+  if (bpart) {  // k / v bias gradient partials: column sums of this workgroup's dK, dV rows
+    const float vs = DROP ? dscale : 1.0f;
+    float* red = (float*)smem;  // [wave][dK 64 | dV 64]; the ring is idle after the last barrier
+    colsum_acc(dk0, dk1, scale, kok, red, 128, 0, wave, lane);
+    colsum_acc(dv0, dv1, vs, kok, red, 128, 64, wave, lane);
+    __syncthreads();
+    if (tid < 128 && (tid & 63) < hd) {
+      const float v = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
+      bpart[((long long)b * gridDim.y + ktile) * ldp + (tid < 64 ? koff + tid : voff + tid - 64)] = v;
+    }
+  }
 }
 
 // ----------------------------------------------------------------------------
@@ -871,7 +916,7 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
                                        long long ldy, const bf16_t* dy, long long lddy, const float* lse,
                                        float* delta, bf16_t* dqkv, long long lddq, int B, int T, int H, int KV,
                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale, float scale,
-                                       const uint32_t* dmask, hipStream_t s) {
+                                       const uint32_t* dmask, float* bpart, long long ldp, hipStream_t s) {
   dim3 gq(B * H, cg_cdiv(T, 128));
   const int wpr = attn_drop_wpr(T);
   const int mode = thr ? (dmask ? 2 : 1) : 0;
@@ -879,7 +924,7 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_begin(CG_PROBE_ATTN_DQ, s);
 #define DQ(D, HDv)                                                                                             \
   hipLaunchKernelGGL((attn_bwd_dq_mfma<D, HDv>), gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse, \
-                     delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr)
+                     delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
 #define DQH(D) if (hd == 64) DQ(D, 64); else if (hd == 48) DQ(D, 48); else DQ(D, 32)
   if (mode == 2) { DQH(2); } else if (mode == 1) { DQH(1); } else { DQH(0); }
 #undef DQH
@@ -891,7 +936,7 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
 #define DKDV(D, HDv)                                                                                            \
   hipLaunchKernelGGL((attn_bwd_dkdv_mfma<D, HDv>), gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv,  \
-                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr)
+                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
 #define DKH(D) if (hd == 64) DKDV(D, 64); else if (hd == 48) DKDV(D, 48); else DKDV(D, 32)
   if (mode == 2) { DKH(2); } else if (mode == 1) { DKH(1); } else { DKH(0); }
 #undef DKH

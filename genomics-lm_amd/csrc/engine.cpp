@@ -224,6 +224,7 @@ struct Acts {
   void* head2;  // bf16 mode: the head weight stacked twice [E; E] (2Vp x d), K operand of the split-dlogits dX
   long long ldl;  // dlogits row stride: Vp, or 2 Vp for split bf16 (hi | lo)
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
+  float* bpart;  // qkv bias-gradient partials from the attention backward [B*ceil(T/128)][Nqkv]
   size_t splitws_floats;
   bool wT;  // transposed weight copies present
   // auxiliary offset heads: pre-GELU a, GELU output g, projection pj (compute dtype, M x d)
@@ -291,6 +292,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.lnpart = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
   const long long maxcols = std::max<long long>({big, (long long)d, (long long)D.Hp});
   A.colws = w.take<float>((size_t)64 * maxcols * 4);
+  A.bpart = w.take<float>((size_t)B * ((T + 127) / 128) * D.Nqkv * 4);
   long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,
                                         (long long)D.Vp * d, (long long)d * d});
   A.splitws_floats = (size_t)MAX_SPLIT * wmax;
@@ -648,6 +650,39 @@ extern "C" size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T
   return carve(cfg, D, B, T, nullptr, A);
 }
 
+// The attention keep-bit arrays depend only on (seed, layer, B, T, H): all layers' arrays are
+// generated on a side stream at the start of the forward, concurrently with the embedding, the
+// LayerNorms and the GEMMs of the first layers (pure-VALU work beside MFMA / DMA-bound kernels);
+// layer l's attention waits on its event.  The side stream first waits for everything already
+// on the caller's stream (the previous backward still reads the arrays).  Off by default
+// (CG_ATTN_MASK_SIDE=1 enables it): measured at C4 it made the step 0.07 ms SLOWER (8.875 vs
+// 8.80 ms, same box) -- the generator's small workgroups delay the dispatch of the main stream's
+// persistent GEMMs more than their VALU work hides beside them.  Default: in order, just before
+// each layer's attention.
+struct MaskStream {
+  hipStream_t s = nullptr;
+  hipEvent_t start = nullptr;
+  std::vector<hipEvent_t> done;
+};
+static MaskStream* mask_stream(int layers) {
+  static const bool on = [] { const char* e = getenv("CG_ATTN_MASK_SIDE"); return e && atoi(e) != 0; }();
+  static MaskStream per_dev[16];
+  if (!on) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
+  MaskStream& ms = per_dev[dev];
+  if (!ms.s) {
+    if (hipStreamCreateWithFlags(&ms.s, hipStreamNonBlocking) != hipSuccess) return ms.s = nullptr, nullptr;
+    if (hipEventCreateWithFlags(&ms.start, hipEventDisableTiming) != hipSuccess) return nullptr;
+  }
+  while ((int)ms.done.size() < layers) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    ms.done.push_back(e);
+  }
+  return &ms;
+}
+
 extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, int B, int T, int training,
                                 uint32_t seed, int window, float* logits, float* loss, void* stream) {
   if (!m || !idx || B <= 0 || T <= 0) return CG_EINVAL;
@@ -669,6 +704,16 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   const float eps = m->cfg.ln_eps > 0 ? m->cfg.ln_eps : 1e-5f;
   m->logits = logits ? logits : A.logits_int;
 
+  const bool masks = p > 0.f && D.L > 0 && A.la[0].dmask;
+  MaskStream* ms = masks ? mask_stream(D.L) : nullptr;
+  if (ms) {
+    if (hipEventRecord(ms->start, C.s) != hipSuccess || hipStreamWaitEvent(ms->s, ms->start, 0) != hipSuccess)
+      return CG_ELAUNCH;
+    for (int l = 0; l < D.L; ++l) {
+      CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, A.la[l].dmask, ms->s));
+      if (hipEventRecord(ms->done[l], ms->s) != hipSuccess) return CG_ELAUNCH;
+    }
+  }
   CK(cg_segment_starts(idx, A.seg, B, T, m->cfg.sep_id, C.s));
   CK(cg_embed_fwd(idx, P(C, C.Lo.tok), C.Lo.pos >= 0 ? P(C, C.Lo.pos) : nullptr, A.x, B, T, d,
                   site_seed(seed, -1, SITE_EMB), p, C.s));
@@ -683,7 +728,11 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     CK(cg_gemm(&g, C.s));
     if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
     const void* dmask = p > 0.f ? a.dmask : nullptr;
-    if (dmask) CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+    if (dmask && ms) {
+      if (hipStreamWaitEvent(C.s, ms->done[l], 0) != hipSuccess) return CG_ELAUNCH;
+    } else if (dmask) {
+      CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+    }
     CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
                    window, site_seed(seed, l, SITE_ATTN), p, dmask, C.s));
     g = lin_fwd(C, a.y, d, o.wp, d, d, d, a.xmid, d);
@@ -854,12 +903,27 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // ---------------- attention branch
     cg_gemm_desc g = lin_dx(C, sl.gattn, d, o.wp, d, d, d, A.dsmall, d, a.pT);
     CK(cg_gemm(&g, C.s));
-    CK(cg_attn_bwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, A.dsmall, d, a.lse, sl.dqkv,
-                   D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p,
-                   p > 0.f ? a.dmask : nullptr, A.delta, C.s));
+    // the qkv bias gradient = column sums of the (un-rotated) dqkv: produced by the MFMA attention
+    // backward itself as per-tile partials when no RoPE rotation follows, else a colsum pass
+    const void* segp = m->cfg.sep_id >= 0 ? A.seg : nullptr;
+    const void* dmask_b = p > 0.f ? a.dmask : nullptr;
+    int rc = CG_EUNSUPPORTED;
+    if (!D.rope)
+      rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
+                       C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, A.bpart, D.Nqkv,
+                       A.delta, C.s);
+    const bool fused_bias = rc == CG_OK;
+    if (rc == CG_EUNSUPPORTED)
+      rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
+                       C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, nullptr, 0,
+                       A.delta, C.s);
+    CK(rc);
     if (D.rope)
       CK(cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
-    CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
+    if (fused_bias)
+      CK(cg_colsum_reduce(A.bpart, C.B * ((C.T + 127) / 128), D.Nqkv, G(C, o.bqkv), accumulate, C.s));
+    else
+      CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
     g = lin_dx(C, sl.dqkv, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
     CK(cg_gemm(&g, C.s));
     // the group's weight gradients once its lowest block is done

@@ -148,12 +148,16 @@ int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
  * same seed and p, or NULL to hash in the kernels (identical keep decisions). */
 size_t cg_attn_drop_mask_bytes(int B, int T, int H);
 int cg_attn_drop_mask(int B, int T, int H, uint32_t drop_seed, float drop_p, void* mask, void* stream);
-/* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: cg_attn_bwd_workspace() */
+/* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: cg_attn_bwd_workspace().
+ * bias_part (optional, bf16 MFMA path only -- CG_EUNSUPPORTED otherwise): fp32 column sums of
+ * dqkv (before bf16 rounding) per (batch, 128-row tile), rows b*ceil(T/128) + tile, leading dim
+ * ld_part >= (H + 2 KV) hd; reduced by cg_colsum_reduce into the q/k/v bias gradients. */
 size_t cg_attn_bwd_workspace(int B, int T, int H);
 int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
                 const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
                 void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
-                uint32_t drop_seed, float drop_p, const void* drop_mask, void* ws, void* stream);
+                uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
+                long long ld_part, void* ws, void* stream);
 
 /* Label-smoothed, class-weighted, ignore_index cross-entropy fwd+bwd over logits rows
  * (F.cross_entropy at model_tiny_gpt.py:343-349).  logits fp32 [rows][ldl], V used

@@ -256,6 +256,29 @@ def test_gemm_dw_grouped_tiles(tile):
         assert err <= 1e-5, (tile, tuple(out.shape), err)
 
 
+@pytest.mark.parametrize("B,T,H,KV,hd,p", [(2, 1024, 8, 8, 64, 0.1), (2, 200, 4, 2, 48, 0.0), (1, 130, 2, 1, 32, 0.1)])
+def test_attention_bwd_bias_partials(B, T, H, KV, hd, p):
+    """The q/k/v bias-gradient partials written by the MFMA attention backward reduce to the
+    column sums of its dqkv (fp32 sums of the unrounded values vs sums of the bf16 output:
+    within bf16 rounding of the rows, rel <= 2e-3 of the column-sum scale)."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(T + hd)
+    N = (H + 2 * KV) * hd
+    qkv = _bf(torch.randn(B * T, N, generator=g)).to(DEV, torch.bfloat16)
+    idx = torch.randint(4, 68, (B, T), generator=g)
+    idx[0, T // 2] = 3
+    seg = ops.segment_starts(idx.to(DEV), 3)
+    y, lse = ops.attn_fwd(qkv, seg, B, T, H, KV, hd, drop_seed=5, drop_p=p)
+    dy = _bf(torch.randn(B * T, H * hd, generator=g)).to(DEV, torch.bfloat16)
+    nrb = B * ((T + 127) // 128)
+    part = torch.full((nrb, N + 8), float("nan"), device=DEV)
+    dqkv = ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, KV, hd, drop_seed=5, drop_p=p, bias_part=part)
+    got = part[:, :N].sum(0)
+    ref = dqkv.float().sum(0)
+    assert torch.isfinite(got).all()
+    assert float((got - ref).abs().max() / ref.abs().max()) <= 2e-3
+
+
 def _mask_bits(words, T):
     """Unpack attn_drop_mask words [BH, T, wpr] (pair-split order) into bool [BH, T, T]."""
     w = words.cpu().numpy().view(np.uint32)
