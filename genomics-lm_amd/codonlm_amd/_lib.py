@@ -117,6 +117,7 @@ SIGNATURES = {
     "cg_attn_fwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp, vp]),
     "cg_attn_drop_mask_bytes": (sz, [i32, i32, i32]),
     "cg_attn_drop_mask": (i32, [i32, i32, i32, u32, f32, vp, vp]),
+    "cg_attn_probs": (i32, [i32, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
                           u32, f32, vp, vp, i64, vp, vp]),
@@ -152,6 +153,7 @@ SIGNATURES = {
     "cg_attn_decode": (i32, [i32, vp, i64, vp, i64, i32, i32, vp, i32, i32, i32, i32, i32, vp, i64, vp]),
     "cg_segstate_step": (i32, [vp, i32, i32, i32, vp, vp]),
     "cg_model_hidden": (vp, [C.POINTER(Model), i32, C.POINTER(i32), C.POINTER(i64)]),
+    "cg_model_attn_probs": (i32, [C.POINTER(Model), i32, vp, vp]),
     "cg_probe_enable": (i32, [i32]),
     "cg_probe_sample": (i32, [i32]),
     "cg_probe_read": (i32, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)]),

@@ -260,6 +260,15 @@ class Engine:
         if bucket_hook:
             bucket_hook("embed")
 
+    def attn_probs(self, layer: int) -> torch.Tensor:
+        """Attention probabilities of block `layer` of the last forward: fp32 (B, H, T, T)."""
+        B, T, H = self.model.B, self.model.T, self.cfg.n_head
+        dev = self.flat.device
+        out = torch.empty(B, H, T, T, dtype=torch.float32, device=dev)
+        L.check(L.lib.cg_model_attn_probs(C.byref(self.model), int(layer), out.data_ptr(), L.stream_ptr(dev)),
+                "cg_model_attn_probs")
+        return out
+
     def hidden(self, which: int) -> torch.Tensor:
         dt = C.c_int(0)
         ld = C.c_longlong(0)

@@ -443,6 +443,16 @@ class TinyGPT(nn.Module):
             m = m & (seg.unsqueeze(-1) == seg.unsqueeze(-2)).unsqueeze(1)
         return m
 
+    def _capture_attention(self):
+        """`blocks[i].attn.last_attn` (B, H, T, T): the softmax probabilities before dropout, as the
+        reference's manual attention path records them (model_tiny_gpt.py:128).  Opt-in here
+        (`model.capture_attn = True`, any attention path): materialising B*H*T^2 floats per block
+        is an inspection cost the training path does not pay."""
+        if not getattr(self, "capture_attn", False):
+            return
+        for i, blk in enumerate(self.blocks):
+            blk.attn.last_attn = self.engine.attn_probs(i)
+
     def next_dropout_seed(self) -> int:
         self._dropout_seed = (self._dropout_seed + 0x9E3779B9) & 0xFFFFFFFF
         return mix_seed_rank(self._dropout_seed, self._seed_rank)
@@ -457,6 +467,7 @@ class TinyGPT(nn.Module):
         training = self.training and self.dropout_p > 0
         seed = self.next_dropout_seed() if training else 0
         logits, loss = eng.forward(idx, targets, training=training, seed=seed, window=attention_window)
+        self._capture_attention()
         if loss is not None and self.training and torch.is_grad_enabled():
             loss = _EngineBackward.apply(loss, self.tok_emb.weight, self)
         if return_aux:

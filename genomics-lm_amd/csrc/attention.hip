@@ -263,6 +263,58 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_vec(const T* __restrict__ qk
 #include "attention_mfma.h"
 
 // ---------------------------------------------------------------------------
+// Attention probabilities of one layer, materialised (the manual path's `last_attn`,
+// model_tiny_gpt.py:117-128: softmax(QK^T/sqrt(hd) masked), before dropout) from the forward's
+// qkv rows and LSE: p = exp(S*scale - lse) on visible (query, key), 0 elsewhere.  Inspection
+// path (B*H*T^2 outputs): one workgroup per (b, h, query) row, the query row in LDS.
+// ---------------------------------------------------------------------------
+template <typename T_>
+__global__ __launch_bounds__(256) void attn_probs_kernel(const T_* __restrict__ qkv, long long ld,
+                                                         const int32_t* __restrict__ seg, const float* __restrict__ lse,
+                                                         float* __restrict__ out, int T, int H, int KV, int hd,
+                                                         int window, float scale) {
+  __shared__ float qs[AV_HD];
+  const long long row = blockIdx.x;  // (b*H + h)*T + q
+  const int q = (int)(row % T);
+  const long long bh = row / T;
+  const int b = (int)(bh / H), h = (int)(bh % H), kvh = h / (H / KV);
+  const long long rb = (long long)b * T;
+  for (int dd = threadIdx.x; dd < hd; dd += blockDim.x) qs[dd] = ld_act<T_>(qkv + (rb + q) * ld + (long long)h * hd + dd);
+  __syncthreads();
+  int lo = seg ? seg[rb + q] : 0;
+  if (window > 0) lo = max(lo, q - window + 1);
+  const float l = lse[row];
+  for (int k = threadIdx.x; k < T; k += blockDim.x) {
+    float p = 0.f;
+    if (k <= q && k >= lo) {
+      const T_* kr = qkv + (rb + k) * ld + (long long)(H + kvh) * hd;
+      float sdot = 0.f;
+      for (int dd = 0; dd < hd; ++dd) sdot = fmaf(qs[dd], ld_act<T_>(kr + dd), sdot);
+      p = __expf(sdot * scale - l);
+    }
+    out[row * T + k] = p;
+  }
+}
+
+extern "C" int cg_attn_probs(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const float* lse,
+                             float* out, int B, int T, int H, int KV, int hd, int window, void* stream) {
+  if (KV <= 0 || H % KV || !qkv || !lse || !out) return CG_EINVAL;
+  if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
+  if (B == 0 || T == 0) return CG_OK;
+  const float scale = 1.0f / sqrtf((float)hd);
+  const dim3 g((unsigned)((long long)B * H * T));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == CG_BF16)
+    hipLaunchKernelGGL(attn_probs_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)qkv, ldqkv, segstart, lse, out, T,
+                       H, KV, hd, window, scale);
+  else
+    hipLaunchKernelGGL(attn_probs_kernel<float>, g, dim3(256), 0, s, (const float*)qkv, ldqkv, segstart, lse, out, T,
+                       H, KV, hd, window, scale);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
+// ---------------------------------------------------------------------------
 // host entry points
 // ---------------------------------------------------------------------------
 extern "C" size_t cg_attn_drop_mask_bytes(int B, int T, int H) {

@@ -952,6 +952,17 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   return CG_EINVAL;
 }
 
+// attention probabilities of block `layer` of the last forward (fp32 [B][H][T][T])
+extern "C" int cg_model_attn_probs(const cg_model* m, int layer, float* out, void* stream) {
+  if (!m || !out) return CG_EINVAL;
+  Ctx C;
+  CK(make_ctx(m, m->B, m->T, stream, C));
+  if (layer < 0 || layer >= C.D.L) return CG_EINVAL;
+  const auto& a = C.A.la[layer];
+  return cg_attn_probs(C.dt, a.qkv, C.D.Nqkv, m->cfg.sep_id >= 0 ? C.A.seg : nullptr, a.lse, out, C.B, C.T, C.D.H,
+                       C.D.KV, C.D.hd, m->window, C.s);
+}
+
 extern "C" const void* cg_model_hidden(const cg_model* m, int which, int* dtype_out, long long* ld) {
   if (!m) return nullptr;
   Ctx C;

@@ -148,6 +148,11 @@ int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
  * same seed and p, or NULL to hash in the kernels (identical keep decisions). */
 size_t cg_attn_drop_mask_bytes(int B, int T, int H);
 int cg_attn_drop_mask(int B, int T, int H, uint32_t drop_seed, float drop_p, void* mask, void* stream);
+/* Attention probabilities materialised (the manual path's `last_attn`, model_tiny_gpt.py:117-128):
+ * out fp32 [B][H][T][T] = exp(S/sqrt(hd) - lse) on visible (query, key), 0 elsewhere, from the
+ * forward's qkv rows (post-RoPE) and lse.  Inspection path. */
+int cg_attn_probs(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const float* lse,
+                  float* out, int B, int T, int H, int KV, int hd, int window, void* stream);
 /* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: cg_attn_bwd_workspace().
  * bias_part (optional, bf16 MFMA path only -- CG_EUNSUPPORTED otherwise): fp32 column sums of
  * dqkv (before bf16 rounding) per (batch, 128-row tile), rows b*ceil(T/128) + tile, leading dim
@@ -348,6 +353,8 @@ int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* s
 /* pointer to hidden state `which` (0 = embedding output, 1..L = block outputs,
  * L+1 = ln_f output) inside the workspace after a forward; dtype in *dtype_out */
 const void* cg_model_hidden(const cg_model* m, int which, int* dtype_out, long long* ld);
+/* attention probabilities of block `layer` of the last forward: fp32 [B][H][T][T] (cg_attn_probs) */
+int cg_model_attn_probs(const cg_model* m, int layer, float* out, void* stream);
 
 /* Incremental decoding with a KV cache (query_model.py generate / next_token :160-214 without
  * re-running the whole prefix).  The cache holds, per layer and sequence, the post-RoPE K and

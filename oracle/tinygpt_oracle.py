@@ -285,7 +285,7 @@ def _to_t(params: dict, requires_grad: bool) -> dict:
     return out
 
 
-def _block(cfg, P, i, x, mask, cos_sin, drop, training):
+def _block(cfg, P, i, x, mask, cos_sin, drop, training, attn_out=None):
     p = f"blocks.{i}."
     B, T, d = x.shape
     H, KV, hd = cfg.n_head, cfg.kv_heads, cfg.head_dim
@@ -305,6 +305,8 @@ def _block(cfg, P, i, x, mask, cos_sin, drop, training):
     att = (q @ k.transpose(-2, -1)) / math.sqrt(hd)
     att = att.masked_fill(~mask[:, None], float("-inf"))
     att = torch.softmax(att, dim=-1)
+    if attn_out is not None:  # the manual path's `last_attn` (model_tiny_gpt.py:128), before dropout
+        attn_out.append(att.detach().clone())
     if training and cfg.dropout > 0 and drop is not None:
         att = att * drop(i, SITE_ATTN, att.shape)
     y = (att @ v).transpose(1, 2).reshape(B, T, d)
@@ -390,6 +392,22 @@ def forward(cfg: OracleConfig, params: dict, idx, targets=None, *, training=Fals
                 w = None
         out["loss"] = cross_entropy(logits.reshape(-1, cfg.vocab_size), tg.reshape(-1),
                                     cfg.label_smoothing, w)
+    return out
+
+
+def attention_probs(cfg: OracleConfig, params: dict, idx, attention_window=None) -> list:
+    """Per-block softmax probabilities (B, H, T, T) of an eval forward -- the reference's
+    `last_attn` (model_tiny_gpt.py:117-128)."""
+    P = _to_t(params, False)
+    idx = torch.as_tensor(np.asarray(idx), dtype=torch.long)
+    B, T = idx.shape
+    with torch.no_grad():
+        x = embed(cfg, P, idx, None, False)
+        mask = attention_mask(idx, cfg.sep_id, attention_window)
+        cos_sin = rope_cos_sin(T, cfg.head_dim) if cfg.use_rope else None
+        out = []
+        for i in range(cfg.n_layer):
+            x = _block(cfg, P, i, x, mask, cos_sin, None, False, attn_out=out)
     return out
 
 

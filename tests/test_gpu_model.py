@@ -62,6 +62,28 @@ def test_fp32_forward_matches_reference(case):
     assert not np.any(diff & (g["top2_margin"] > 1e-3 * scale)), int(diff.sum())
 
 
+@pytest.mark.parametrize("case,dtype", [("mha_gelu_sep", "fp32"), ("gqa_rope_swiglu_w", "fp32"),
+                                        ("window8", "fp32"), ("hd48_gqa", "bf16")])
+def test_last_attn_capture(case, dtype):
+    """model.capture_attn = True records blocks[i].attn.last_attn (B, H, T, T), the softmax
+    probabilities before dropout (reference manual path, model_tiny_gpt.py:128), against the
+    oracle's (SEP segments, RoPE + GQA, local window; fp32 1e-5, bf16 operands 2e-2)."""
+    cfgd, g = load_golden(case)
+    m, cfg, params = make_model(cfgd, g, dtype=dtype)
+    m.eval()
+    m.capture_attn = True
+    x, _ = _idx(g)
+    window = 8 if case == "window8" else None
+    with torch.no_grad():
+        m(x, attention_window=window)
+    ref = O.attention_probs(cfg, params, g["idx"], attention_window=window)
+    tol = 1e-5 if dtype == "fp32" else 2e-2
+    for i, blk in enumerate(m.blocks):
+        got = blk.attn.last_attn.cpu()
+        assert got.shape == ref[i].shape
+        assert float((got - ref[i]).abs().max()) <= tol, (i, float((got - ref[i]).abs().max()))
+
+
 @pytest.mark.parametrize("case", ["mha_gelu_sep", "gqa_rope_swiglu_w", "untied_causal", "hd48_gqa"])
 def test_fp32_grads_match_reference(case):
     cfgd, g = load_golden(case)
