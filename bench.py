@@ -150,7 +150,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
-    ap.add_argument("--path", default="engine", choices=["engine", "trainer"])
+    ap.add_argument("--path", default="engine", choices=["engine", "trainer", "forward"],
+                    help="engine: the DP training step; trainer: the trainer's per-microbatch sequence; "
+                         "forward: the eval-mode batched forward of extract_embeddings / query_model")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -217,7 +219,16 @@ def main():
             total = total + 0.1 * obj.termination_aux_loss(auxo["termination_logits"], labels)
         return total
 
-    if args.path == "engine" and not aux:
+    fwd_only = args.path == "forward"
+    if fwd_only:
+        model.eval()
+
+        def run(i):
+            xb, _ = batches[i % nbuf]
+            with torch.no_grad():
+                logits, _ = model(xb)
+            return logits[:1, :1].float().sum()
+    elif args.path == "engine" and not aux:
         def run(i):
             xb, yb = batches[i % nbuf]
             return stepper.step(xb, yb, seed=1000 + i)
@@ -305,10 +316,15 @@ def main():
 
     tokens = world * B * T * args.steps
     value = tokens / elapsed
-    ftok = flops_per_token(c)
+    ftok = flops_per_token(c) // (3 if fwd_only else 1)  # a forward is one third of a training step
+    if fwd_only:
+        metric = f"codon tokens/sec batched forward (eval, {args.config})"
+    elif args.config == "c4":
+        metric = "codon tokens/sec training step, 12L8H d512 seq1024"
+    else:
+        metric = f"codon tokens/sec training step ({args.config})"
     result = {
-        "metric": "codon tokens/sec training step, 12L8H d512 seq1024" if args.config == "c4"
-        else f"codon tokens/sec training step ({args.config})",
+        "metric": metric,
         "value": round(value, 1),
         "unit": "tokens/s",
         "n_gpus": world,
@@ -320,11 +336,14 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (uniform random codons 4..67, resident in HBM; random-init weights)",
-        "config": {"workload": f"TinyGPT {c['n_layer']}L{c['n_head']}H d{c['n_embd']} T{T} V68 train step"
-                               + (" + 5 offset heads + termination head (trainer objective)" if aux else ""),
+        "config": {"workload": f"TinyGPT {c['n_layer']}L{c['n_head']}H d{c['n_embd']} T{T} V68 "
+                               + ("eval forward" if fwd_only else "train step")
+                               + (" + 5 offset heads + termination head (trainer objective)" if aux and not fwd_only
+                                  else ""),
                    "model": "TinyGPT (genomics-lm src/codonlm)", "global_batch": world * B, "seq_len": T,
                    "micro_batch_per_gpu": B, "parallelism": f"dp{world}", "dropout": 0.1,
-                   "label_smoothing": 0.05, "sep_mask": True, "path": args.path if not aux else "trainer"},
+                   "label_smoothing": 0.05, "sep_mask": True,
+                   "path": args.path if (not aux or fwd_only) else "trainer"},
         "final_loss": round(final_loss, 4),
         "model_flops_per_token": ftok,
         "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),

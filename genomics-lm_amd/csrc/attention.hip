@@ -17,6 +17,7 @@
 
 constexpr int AV_HD = 64;   // max head dim of the vector kernels
 constexpr int AV_TQ = 64;   // queries (or keys) per block
+constexpr int AV_SUB = 16;  // keys per online-softmax update in the forward
 
 __device__ __forceinline__ bool attn_visible(int q, int j, int lo) { return j <= q && j >= lo; }
 
@@ -26,8 +27,10 @@ __global__ __launch_bounds__(64) void attn_fwd_vec(const T* __restrict__ qkv, lo
                                                    long long ldy, float* __restrict__ lse, int Tn, int H, int KV,
                                                    int hd, int window, uint32_t seed, uint32_t thr, float dscale,
                                                    float scale) {
-  __shared__ float Ks[AV_TQ][AV_HD + 1];
-  __shared__ float Vs[AV_TQ][AV_HD + 1];
+  // every lane reads the same K/V row (broadcast): rows unpadded and 16-B aligned so the reads
+  // are ds_read_b128 (4 FMAs per LDS read instead of 1)
+  __shared__ __attribute__((aligned(16))) float Ks[AV_TQ][AV_HD];
+  __shared__ __attribute__((aligned(16))) float Vs[AV_TQ][AV_HD];
   const int lane = threadIdx.x;
   const int bh = blockIdx.y, b = bh / H, h = bh % H, kvh = h / (H / KV);
   const int q = blockIdx.x * AV_TQ + lane;
@@ -60,33 +63,51 @@ __global__ __launch_bounds__(64) void attn_fwd_vec(const T* __restrict__ qkv, lo
       Vs[j][d] = ok ? ld_act<T>(qkv + kr + voff + d) : 0.f;
     }
     __syncthreads();
-    float s[AV_TQ];
-    float mt = -INFINITY;
+    // keys in sub-tiles of AV_SUB with an online-softmax update each: the score row stays in
+    // registers (a whole 64-key row unrolled makes hipcc hoist every K read and spill)
+#pragma unroll 1
+    for (int jb = 0; jb < AV_TQ; jb += AV_SUB) {
+      float s[AV_SUB];
+      float mt = -INFINITY;
 #pragma unroll
-    for (int j = 0; j < AV_TQ; ++j) {
-      const int key = k0 + j;
-      float acc = 0.f;
+      for (int jj = 0; jj < AV_SUB; ++jj) {
+        const int j = jb + jj, key = k0 + j;
+        float acc = 0.f;
 #pragma unroll
-      for (int d = 0; d < AV_HD; ++d) acc += qv[d] * Ks[j][d];
-      const bool vis = qok && key < Tn && attn_visible(q, key, lo);
-      s[j] = vis ? acc * scale : -INFINITY;
-      mt = fmaxf(mt, s[j]);
+        for (int d = 0; d < AV_HD; d += 4) {
+          const float4 k4 = *(const float4*)&Ks[j][d];
+          acc = fmaf(qv[d], k4.x, acc);
+          acc = fmaf(qv[d + 1], k4.y, acc);
+          acc = fmaf(qv[d + 2], k4.z, acc);
+          acc = fmaf(qv[d + 3], k4.w, acc);
+        }
+        const bool vis = qok && key < Tn && attn_visible(q, key, lo);
+        s[jj] = vis ? acc * scale : -INFINITY;
+        mt = fmaxf(mt, s[jj]);
+      }
+      const float mn = fmaxf(m, mt);
+      if (mn == -INFINITY) continue;
+      const float alpha = __expf(m - mn);
+      l *= alpha;
+#pragma unroll
+      for (int d = 0; d < AV_HD; ++d) o[d] *= alpha;
+#pragma unroll
+      for (int jj = 0; jj < AV_SUB; ++jj) {
+        const int j = jb + jj;
+        float p = __expf(s[jj] - mn);
+        l += p;
+        if (thr) p = cg_keep(seed, drow, (uint32_t)(k0 + j), thr) ? p * dscale : 0.f;
+#pragma unroll
+        for (int d = 0; d < AV_HD; d += 4) {
+          const float4 v4 = *(const float4*)&Vs[j][d];
+          o[d] = fmaf(p, v4.x, o[d]);
+          o[d + 1] = fmaf(p, v4.y, o[d + 1]);
+          o[d + 2] = fmaf(p, v4.z, o[d + 2]);
+          o[d + 3] = fmaf(p, v4.w, o[d + 3]);
+        }
+      }
+      m = mn;
     }
-    const float mn = fmaxf(m, mt);
-    if (mn == -INFINITY) continue;
-    const float alpha = __expf(m - mn);
-    l *= alpha;
-#pragma unroll
-    for (int d = 0; d < AV_HD; ++d) o[d] *= alpha;
-#pragma unroll
-    for (int j = 0; j < AV_TQ; ++j) {
-      float p = __expf(s[j] - mn);
-      l += p;
-      if (thr) p = cg_keep(seed, drow, (uint32_t)(k0 + j), thr) ? p * dscale : 0.f;
-#pragma unroll
-      for (int d = 0; d < AV_HD; ++d) o[d] += p * Vs[j][d];
-    }
-    m = mn;
   }
   if (qok) {
     const float il = 1.0f / l;

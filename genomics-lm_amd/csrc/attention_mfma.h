@@ -329,6 +329,10 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
         s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 32, ks, lane), qf[ks], s1, 0, 0, 0);
       }
     }
+    // S feeds inline asm (max3): hipcc pads the XDL-result -> VALU-read hazard only before its own
+    // instructions, so the accumulators pass through a wait of 19 states here (>= the 16-pass
+    // rule); without it v_max3 can read a stale accumulator and the row max varies run to run
+    asm volatile("s_nop 15\n\ts_nop 2" : "+v"(s0), "+v"(s1));
     if constexpr (!FULL) {
       const int kq = myq - k0, kl = lo - k0;  // visible iff kl <= key-k0 <= kq
 #pragma unroll
