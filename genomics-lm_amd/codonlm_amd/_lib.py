@@ -59,6 +59,18 @@ class DwGroup(C.Structure):
     _fields_ = [("n", i32), ("K", i32), ("tile_m", i32), ("p", DwProduct * DW_MAX)]
 
 
+REDUCE_MAX = 48
+
+
+class ReduceJob(C.Structure):
+    _fields_ = [("part", vp), ("ld", i64), ("nrows", i32), ("cols", i32), ("dst", vp), ("accumulate", i32),
+                ("first_block", i32)]
+
+
+class ReduceBatch(C.Structure):
+    _fields_ = [("n", i32), ("j", ReduceJob * REDUCE_MAX)]
+
+
 class AdamwSegment(C.Structure):
     _fields_ = [("begin", i64), ("end", i64), ("lr", f32), ("wd", f32)]
 
@@ -109,6 +121,9 @@ SIGNATURES = {
     "cg_layernorm_bwd_blocks": (i32, [i32]),
     "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, vp, vp,
                                vp, i32, i32, i32, f32, vp]),
+    "cg_layernorm_bwd_partials": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, i32,
+                                        i32, i32, vp]),
+    "cg_reduce_columns": (i32, [C.POINTER(ReduceBatch), vp]),
     "cg_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, u32, f32, vp]),
     "cg_embed_bwd_workspace": (sz, [i32, i32, i32, i32]),
     "cg_embed_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, u32, f32, i32, vp, vp]),

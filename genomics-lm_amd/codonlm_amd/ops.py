@@ -111,6 +111,38 @@ def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5, branch_dtype=N
     return g_out, dgamma, dbeta
 
 
+def layernorm_bwd_partials(dy, x, mean, rstd, weight, g_in=None, branch_dtype=None, drop_seed=0, drop_p=0.0):
+    """LayerNorm backward row pass without the parameter reduction (cg_layernorm_bwd_partials):
+    returns (g_out, partials [nblk][(2 + want_col) * cols], branch or None)."""
+    rows, cols = x.shape
+    g_out = torch.empty(rows, cols, dtype=torch.float32, device=x.device)
+    nblk = L.lib.cg_layernorm_bwd_blocks(rows)
+    nw = 3 if branch_dtype is not None else 2
+    part = torch.empty(nblk, nw * cols, dtype=torch.float32, device=x.device)
+    branch = torch.empty(rows, cols, dtype=branch_dtype, device=x.device) if branch_dtype is not None else None
+    L.check(L.lib.cg_layernorm_bwd_partials(_dt(dy), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0),
+                                            mean.data_ptr(), rstd.data_ptr(), weight.data_ptr(), _p(g_in),
+                                            g_out.data_ptr(), _dt(branch) if branch is not None else L.CG_F32,
+                                            _p(branch), drop_seed, drop_p, part.data_ptr(), int(nw == 3), rows, cols,
+                                            L.stream_ptr(x.device)), "cg_layernorm_bwd_partials")
+    return g_out, part, branch
+
+
+def reduce_columns(jobs):
+    """One cg_reduce_columns launch over jobs = [(part 2-D fp32 view, dst fp32 [cols], accumulate)]:
+    dst (+)= part.sum(0) in the kernel's fixed order."""
+    bt = L.ReduceBatch()
+    bt.n = len(jobs)
+    dev = None
+    for i, (part, dst, acc) in enumerate(jobs):
+        j = bt.j[i]
+        j.part = part.data_ptr(); j.ld = part.stride(0); j.nrows = part.shape[0]; j.cols = part.shape[1]
+        j.dst = dst.data_ptr(); j.accumulate = int(acc)
+        dev = part.device
+    L.check(L.lib.cg_reduce_columns(C.byref(bt), L.stream_ptr(dev) if dev is not None else None),
+            "cg_reduce_columns")
+
+
 def segment_starts(idx, sep_id):
     B, T = idx.shape
     out = torch.empty(B, T, dtype=torch.int32, device=idx.device)

@@ -95,6 +95,45 @@ __device__ __forceinline__ v8bf frag_tr(const char* img, int rb, int s, int cb, 
   return __builtin_bit_cast(v8bf, r);
 }
 
+// Per-lane image offsets, computed once per kernel: the XOR swizzle of dual_off depends only on
+// (row >> 1) & 7, so moving a read by 16 rows (or a multiple) moves it by a constant and every
+// frag_row / frag_tr of the tile loops becomes (lane offset + immediate).  Without this hipcc
+// re-derives the swizzled address of each of the ~24 reads per tile (one VALU op each).
+struct RowOff {
+  uint32_t o[4];  // frag_row(img, 0, ks, lane) for ks = 0..3
+};
+struct TrOff {
+  uint32_t o[2][2];  // frag_tr(img, 0, 0, cb, lane): [cb][the lo / hi 8-row half]
+};
+__device__ __forceinline__ RowOff row_offsets(int lane) {
+  RowOff r;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) r.o[ks] = (uint32_t)dual_off(lane & 31, 2 * ks + (lane >> 5));
+  return r;
+}
+__device__ __forceinline__ TrOff tr_offsets(int lane) {
+  const int h = lane >> 5, g16 = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, p = i16 & 3;
+  TrOff t;
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int ch = ((cb * 32 + g16 * 16) >> 3) + (p >> 1);
+    t.o[cb][0] = (uint32_t)(dual_off(4 * h + q, ch) + 8 * (p & 1));
+    t.o[cb][1] = (uint32_t)(dual_off(4 * h + q + 8, ch) + 8 * (p & 1));
+  }
+  return t;
+}
+// rb: multiple of 16 rows
+__device__ __forceinline__ v8bf frag_row_o(const char* img, const RowOff& ro, int rb, int ks) {
+  return *(const v8bf*)(img + ro.o[ks] + rb * 128);
+}
+__device__ __forceinline__ v8bf frag_tr_o(const char* img, const TrOff& to, int rb, int s, int cb) {
+  const int d = (rb + 16 * s) * 128;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + to.o[cb][0] + d));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + to.o[cb][1] + d));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
+
 typedef float v2f_a __attribute__((ext_vector_type(2)));
 typedef __bf16 v2bf_a __attribute__((ext_vector_type(2)));
 typedef uint32_t v4u_a __attribute__((ext_vector_type(4)));
@@ -133,6 +172,12 @@ __device__ __forceinline__ float keep_f(float v, uint32_t w, int bit) {
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "i"(bit));
   return __int_as_float(__float_as_int(v) & m);
 }
+// all-ones / zero from constant bit `bit` of w
+__device__ __forceinline__ int keep_mask_i(uint32_t w, int bit) {
+  int m;
+  asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "i"(bit));
+  return m;
+}
 // all-ones / zero from bit `pos` (a per-lane register) of w
 __device__ __forceinline__ int keep_mask(uint32_t w, uint32_t pos) {
   int m;
@@ -157,6 +202,21 @@ __device__ __forceinline__ v8bf pack_b_keep(const v16f& x, int s, uint32_t w) {
   return __builtin_bit_cast(v8bf, v);
 }
 
+// keep bits applied to an already packed B fragment (rows 8s..8s+7 of an accumulator)
+__device__ __forceinline__ v8bf keep_b(v8bf u, int s, uint32_t w) {
+  v4u_a v = __builtin_bit_cast(v4u_a, u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = keep_pk(v[i], w, kbit(8 * s + 2 * i));
+  return __builtin_bit_cast(v8bf, v);
+}
+// A operand of all ones: ones x B sums B over its k rows into every row of the result
+__device__ __forceinline__ v8bf ones_frag() {
+  v8bf o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = (__bf16)1.0f;
+  return o;
+}
+
 // B operand straight from global: row `row` (the lane's column index), k-step ks
 __device__ __forceinline__ v8bf frag_global(const bf16_t* rowp, bool ok, int ks, int hd, int lane) {
   const int c = ks * 16 + 8 * (lane >> 5);
@@ -176,28 +236,34 @@ __device__ __forceinline__ v16f zero16() {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-// sum over the 32 lanes of a half-wave (lanes l and l^32 are summed separately)
-__device__ __forceinline__ float half_sum(float v) {
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
-  v += __shfl_xor(v, 16, 64);
-  return v;
-}
-// The workgroup's 128 rows of two accumulator blocks x0 (columns 0..31) and x1 (32..63), one
-// row per lane-half, summed per column into red[wave][c0 + column] (LDS, 4 waves x stride)
-__device__ __forceinline__ void colsum_acc(const v16f& x0, const v16f& x1, float s, bool ok, float* red, int stride,
-                                           int c0, int wave, int lane) {
+// Column sums over the workgroup's 128 accumulator columns (4 waves x 32 lanes) of the 64 rows
+// held in two accumulator blocks x0 (rows 0..31) and x1 (32..63), for the bias-gradient partials:
+// the values go through LDS ([wave][row][33 lanes], conflict-free stores and reads), each thread
+// sums one (wave, row) run of 32, and threads 0..63 add the 4 waves' sums -- fixed order, no
+// cross-lane shuffle chains.  `red` needs COLSUM_LDS bytes; ends with a barrier (red reusable).
+constexpr int COLSUM_LDS = (4 * 64 * 33 + 4 * 64) * 4;
+__device__ __forceinline__ float colsum_wg(const v16f& x0, const v16f& x1, float s, bool ok, float* red, int wave,
+                                           int lane, int tid) {
+  float* t = red + wave * 64 * 33 + (lane & 31);
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
-    const float v0 = half_sum(ok ? x0[r] * s : 0.f);
-    const float v1 = half_sum(ok ? x1[r] * s : 0.f);
-    if ((lane & 31) == 0) {
-      red[wave * stride + c0 + acc_row(r, lane)] = v0;
-      red[wave * stride + c0 + 32 + acc_row(r, lane)] = v1;
-    }
+    t[acc_row(r, lane) * 33] = ok ? x0[r] * s : 0.f;
+    t[(32 + acc_row(r, lane)) * 33] = ok ? x1[r] * s : 0.f;
   }
+  __syncthreads();
+  const float* run = red + (tid >> 6) * 64 * 33 + (tid & 63) * 33;
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    a += run[k];
+    b += run[k + 1];
+  }
+  float* part = red + 4 * 64 * 33;
+  part[tid] = a + b;
+  __syncthreads();
+  const float v = tid < 64 ? (part[tid] + part[64 + tid]) + (part[128 + tid] + part[192 + tid]) : 0.f;
+  __syncthreads();
+  return v;  // threads 0..63: the column sum of row tid
 }
 
 // visible-key lower bound for query q (monotone non-decreasing in q)
@@ -234,15 +300,17 @@ __device__ __forceinline__ uint32_t shift_in_keep(uint32_t acc, uint32_t h, uint
   return r;
 }
 
-__global__ __launch_bounds__(64) void attn_drop_mask_kernel(uint32_t* __restrict__ qmask, int T, int wpr,
-                                                            uint32_t seed, uint32_t thr) {
-  const int i = blockIdx.x;
+__global__ __launch_bounds__(256) void attn_drop_mask_kernel(uint32_t* __restrict__ qmask, int T, int wpr,
+                                                             uint32_t seed, uint32_t thr, int nbt) {
+  // 4 waves per workgroup, one 64x64 block each (one-wave workgroups were dispatch-bound)
+  const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (i >= nbt) return;
   int qb = (int)((sqrtf(8.f * (float)i + 1.f) - 1.f) * 0.5f);
   while ((qb + 1) * (qb + 2) / 2 <= i) ++qb;
   while (qb * (qb + 1) / 2 > i) --qb;
   const int kb = i - qb * (qb + 1) / 2;
   const long long bh = blockIdx.y;
-  const int q = qb * 64 + (int)threadIdx.x;
+  const int q = qb * 64 + (int)(threadIdx.x & 63);
   if (q >= T) return;
   const uint32_t hrow = cg_row_hash(seed, (uint32_t)(bh * T + q));
   uint32_t wq[2];
@@ -311,50 +379,44 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
   const uint32_t* qm = DROP == 2 ? qmask + ((long long)bh * T + (qok ? myq : 0)) * wpr : nullptr;
   constexpr int nks = (hd + 15) >> 4;
 
-  float m = -INFINITY, lsum = 0.f;
-  v16f o0 = zero16(), o1 = zero16();
+  float m = -INFINITY;
+  // row sums of P accumulate on the MFMA (ones x P, every row of ls = the lane's query sum; only
+  // ls[0] is read or rescaled): 4 MFMAs per tile instead of 32 VALU adds
+  v16f o0 = zero16(), o1 = zero16(), ls = zero16();
+  const RowOff ro = row_offsets(lane);
+  const TrOff to = tr_offsets(lane);
+  const v8bf ones = ones_frag();
   const int t0 = kmin / KT, t1 = kmax / KT;
   tile_dma(lds0, kv, t0 * tstride + kcol, wave_u);
   tile_dma(lds0 + IMG, kv, t0 * tstride + vcol, wave_u);
   dma_drain();
   __syncthreads();
 
-  auto body = [&](const char* Ki, const char* Vi, int k0, uint2 wc, auto full_c) __attribute__((always_inline)) {
+  // One 32-key half of a tile (keys k0 + 32 kb ..): mask, online-softmax update, exp, row sums
+  // and the P.V product of that half.  The tile's two S halves are issued back to back, so the
+  // second half's QK^T MFMAs run while the first half is exponentiated, and the first half's
+  // PV MFMAs while the second is (MFMA/VALU overlap inside one wave).
+  auto half = [&](v16f& sx, const int kb, const char* Vi, int k0, uint32_t wword, auto full_c)
+                  __attribute__((always_inline)) {
     constexpr bool FULL = decltype(full_c)::value;
-    v16f s0 = zero16(), s1 = zero16();
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks < nks) {
-        s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 0, ks, lane), qf[ks], s0, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, 32, ks, lane), qf[ks], s1, 0, 0, 0);
-      }
-    }
-    // S feeds inline asm (max3): hipcc pads the XDL-result -> VALU-read hazard only before its own
-    // instructions, so the accumulators pass through a wait of 19 states here (>= the 16-pass
-    // rule); without it v_max3 can read a stale accumulator and the row max varies run to run
-    asm volatile("s_nop 15\n\ts_nop 2" : "+v"(s0), "+v"(s1));
     if constexpr (!FULL) {
-      const int kq = myq - k0, kl = lo - k0;  // visible iff kl <= key-k0 <= kq
+      const int kq = myq - k0 - 32 * kb, kl = lo - k0 - 32 * kb;  // visible iff kl <= key <= kq
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int j0 = acc_row(r, lane), j1 = j0 + 32;
-        s0[r] = (j0 > kq || j0 < kl) ? -INFINITY : s0[r];
-        s1[r] = (j1 > kq || j1 < kl) ? -INFINITY : s1[r];
+        const int j = acc_row(r, lane);
+        sx[r] = (j > kq || j < kl) ? -INFINITY : sx[r];
       }
     }
-    float ma = max3(s0[0], s0[1], s0[2]), mb = max3(s1[0], s1[1], s1[2]);
+    float ma = max3(sx[0], sx[1], sx[2]);
 #pragma unroll
-    for (int r = 3; r < 15; r += 2) {
-      ma = max3(ma, s0[r], s0[r + 1]);
-      mb = max3(mb, s1[r], s1[r + 1]);
-    }
-    const float mx = max_xhalf(max3(max3(ma, mb, s0[15]), s1[15], s1[15]));
-    // NaN-safe: (-inf) - (-inf) compares false (a fully masked tile never grows m)
+    for (int r = 3; r < 15; r += 2) ma = max3(ma, sx[r], sx[r + 1]);
+    const float mx = max_xhalf(max3(ma, sx[15], sx[15]));
+    // NaN-safe: (-inf) - (-inf) compares false (a fully masked half never grows m)
     const bool grow = (mx - m) * c > 8.0f;
     if (__any(grow)) {
       const float mn = grow ? mx : m;
       const float alpha = grow ? __builtin_amdgcn_exp2f((m - mn) * c) : 1.0f;
-      lsum *= alpha;
+      ls[0] *= alpha;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         o0[r] *= alpha;
@@ -363,48 +425,59 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       m = mn;
     }
     const float mc = (m == -INFINITY ? 0.f : m) * c;
-    float ps = 0.f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], c, -mc));
-      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], c, -mc));
-      ps += s0[r] + s1[r];
-    }
-    lsum += ps;
+    for (int r = 0; r < 16; ++r) sx[r] = __builtin_amdgcn_exp2f(fmaf(sx[r], c, -mc));
+    // the normaliser is the sum of the bf16-rounded P the PV product uses (before the keep bits;
+    // the hash path sums before its fp32 keep test)
     if constexpr (DROP == 1) {
+      ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pack_b(sx, 0), ls, 0, 0, 0);
+      ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pack_b(sx, 1), ls, 0, 0, 0);
       // colpair of (kb, r) = k0/2 + 2*hl + (r&3)/2 + 4*(r>>2) + 16*kb; the 1/(1-p) scale is
       // applied once to O at the end
-      const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl) * CG_COLK;
+      const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl + 16u * (uint32_t)kb) * CG_COLK;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
-        const uint32_t h0 = cg_pair_mix(hb + off * CG_COLK);
-        const uint32_t h1 = cg_pair_mix(hb + (off + 16u) * CG_COLK);
-        s0[r] = (h0 & 0xFFFFu) >= thr ? s0[r] : 0.f;
-        s0[r + 1] = (h0 >> 16) >= thr ? s0[r + 1] : 0.f;
-        s1[r] = (h1 & 0xFFFFu) >= thr ? s1[r] : 0.f;
-        s1[r + 1] = (h1 >> 16) >= thr ? s1[r + 1] : 0.f;
+        const uint32_t h = cg_pair_mix(hb + off * CG_COLK);
+        sx[r] = (h & 0xFFFFu) >= thr ? sx[r] : 0.f;
+        sx[r + 1] = (h >> 16) >= thr ? sx[r + 1] : 0.f;
       }
     }
-    v8bf p00, p01, p10, p11;
+    v8bf pa = pack_b(sx, 0), pb = pack_b(sx, 1);
+    if constexpr (DROP != 1) {
+      ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pa, ls, 0, 0, 0);
+      ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, ls, 0, 0, 0);
+    }
     if constexpr (DROP == 2) {
-      // keys k0 + acc_row(r) (s0) and k0 + 32 + acc_row(r) (s1): words wc.x / wc.y
-      const uint32_t w0 = wc.x >> (2 * hl), w1 = wc.y >> (2 * hl);
-      p00 = pack_b_keep(s0, 0, w0); p01 = pack_b_keep(s0, 1, w0);
-      p10 = pack_b_keep(s1, 0, w1); p11 = pack_b_keep(s1, 1, w1);
-    } else {
-      p00 = pack_b(s0, 0); p01 = pack_b(s0, 1); p10 = pack_b(s1, 0); p11 = pack_b(s1, 1);
+      // keys k0 + 32 kb + acc_row(r): word wword
+      const uint32_t w = wword >> (2 * hl);
+      pa = keep_b(pa, 0, w);
+      pb = keep_b(pb, 1, w);
     }
-    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 0, lane), p00, o0, 0, 0, 0);
-    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 0, lane), p01, o0, 0, 0, 0);
-    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 0, lane), p10, o0, 0, 0, 0);
-    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 0, lane), p11, o0, 0, 0, 0);
+    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 0), pa, o0, 0, 0, 0);
+    o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 0), pb, o0, 0, 0, 0);
     if constexpr (hd > 32) {
-      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 0, 1, lane), p00, o1, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 0, 1, 1, lane), p01, o1, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 0, 1, lane), p10, o1, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Vi, 32, 1, 1, lane), p11, o1, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 1), pa, o1, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 1), pb, o1, 0, 0, 0);
     }
+  };
+  auto body = [&](const char* Ki, const char* Vi, int k0, uint2 wc, auto full_c) __attribute__((always_inline)) {
+    v16f s0 = zero16(), s1 = zero16();
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      if (ks < nks) s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, 0, ks), qf[ks], s0, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // issue order: the s0 chain, then the s1 chain, then half 0
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      if (ks < nks) s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, 32, ks), qf[ks], s1, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    // S feeds inline asm (max3): hipcc pads the XDL-result -> VALU-read hazard only before its own
+    // instructions, so each half's accumulator passes through a wait of 19 states first (>= the
+    // 16-pass rule); without it v_max3 can read a stale accumulator and the row max varies run to run
+    asm volatile("s_nop 15\n\ts_nop 2" : "+v"(s0));
+    half(s0, 0, Vi, k0, wc.x, full_c);
+    asm volatile("s_nop 15\n\ts_nop 2" : "+v"(s1));
+    half(s1, 1, Vi, k0, wc.y, full_c);
   };
   // the keep words are fetched one tile ahead (tiles above the wave's diagonal read words that
   // were never written; their pairs are causally masked)
@@ -433,7 +506,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
     step(std::integral_constant<int, 0>{}, t);
     if (t + 1 <= t1) step(std::integral_constant<int, 1>{}, t + 1);
   }
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float ltot = ls[0];
   if (qok) {
     const float inv = (DROP ? dscale : 1.0f) / ltot;
     bf16_t* yr = y + (rowbase + myq) * ldy + (long long)hh * hd;
@@ -524,15 +597,34 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
   __syncthreads();
   uint2 wn = make_uint2(0, 0);
   if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * t0);
-  for (int t = t0; t <= t1; ++t) {
-    const int cur = (t - t0) & 1;
-    const char* Ki = smem + cur * 2 * IMG;
+  const RowOff ro = row_offsets(lane);
+  const TrOff to = tr_offsets(lane);
+  // dP starts from nd = -delta/dscale, added by one MFMA (ones x [hi; lo] split-bf16 nd rows:
+  // exact to ~2^-16): the accumulator is dP - delta/dscale and dS/dscale = p * (keep ? acc : nd)
+  const float nd = -dl * (DROP ? 1.0f / dscale : 1.0f);
+  v8bf ndfrag, onesk;
+  {
+    const __bf16 hi = (__bf16)nd;
+    const __bf16 lo = (__bf16)(nd - (float)hi);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      ndfrag[j] = (__bf16)0.f;
+      onesk[j] = (__bf16)0.f;
+    }
+    if (lane < 32) {
+      ndfrag[0] = hi; ndfrag[1] = lo;
+      onesk[0] = (__bf16)1.f; onesk[1] = (__bf16)1.f;
+    }
+  }
+  auto step = [&](auto cur_c, int t) __attribute__((always_inline)) {
+    constexpr int CUR = decltype(cur_c)::value;
+    const char* Ki = smem + CUR * 2 * IMG;
     const char* Vi = Ki + IMG;
     const bool more = t < t1;
     const uint2 wc = wn;
     if (more) {  // the other buffer was last read before the previous barrier
-      tile_dma(lds0 + (cur ^ 1) * 2 * IMG, kv, (t + 1) * tstride + kcol, wave_u);
-      tile_dma(lds0 + (cur ^ 1) * 2 * IMG + IMG, kv, (t + 1) * tstride + vcol, wave_u);
+      tile_dma(lds0 + (CUR ^ 1) * 2 * IMG, kv, (t + 1) * tstride + kcol, wave_u);
+      tile_dma(lds0 + (CUR ^ 1) * 2 * IMG + IMG, kv, (t + 1) * tstride + vcol, wave_u);
       if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * (t + 1));
     }
     const int k0 = t * KT;
@@ -543,12 +635,13 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
     auto body = [&](bool full) __attribute__((always_inline)) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        v16f s = zero16(), dp = zero16();
+        v16f s = zero16();
+        v16f dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, ndfrag, zero16(), 0, 0, 0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           if (ks < nks) {
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Ki, kb * 32, ks, lane), qf[ks], s, 0, 0, 0);
-            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Vi, kb * 32, ks, lane), df[ks], dp, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, kb * 32, ks), qf[ks], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Vi, ro, kb * 32, ks), df[ks], dp, 0, 0, 0);
           }
         }
         const int kq = myq - k0 - kb * 32, kl = lo - k0 - kb * 32;
@@ -565,35 +658,39 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
         for (int r = 0; r < 16; r += 2) {
           const float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
           const float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c, -lse2));
-          float d0 = dp[r], d1 = dp[r + 1];
           if constexpr (DROP == 1) {
             const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
             const uint32_t hsh = cg_pair_mix(hb + off * CG_COLK);
-            d0 = (hsh & 0xFFFFu) >= thr ? d0 * dscale : 0.f;
-            d1 = (hsh >> 16) >= thr ? d1 * dscale : 0.f;
-            s[r] = p0 * (d0 - dl);
-            s[r + 1] = p1 * (d1 - dl);
+            s[r] = p0 * ((hsh & 0xFFFFu) >= thr ? dp[r] : nd);
+            s[r + 1] = p1 * ((hsh >> 16) >= thr ? dp[r + 1] : nd);
           } else if constexpr (DROP == 2) {
-            s[r] = p0 * fmaf(keep_f(d0, wb, kbit(r)), dscale, -dl);
-            s[r + 1] = p1 * fmaf(keep_f(d1, wb, kbit(r + 1)), dscale, -dl);
+            const uint32_t m0 = (uint32_t)keep_mask_i(wb, kbit(r)), m1 = (uint32_t)keep_mask_i(wb, kbit(r + 1));
+            s[r] = p0 * __uint_as_float((__float_as_uint(dp[r]) & m0) | (__float_as_uint(nd) & ~m0));
+            s[r + 1] = p1 * __uint_as_float((__float_as_uint(dp[r + 1]) & m1) | (__float_as_uint(nd) & ~m1));
           } else {
-            s[r] = p0 * (d0 - dl);
-            s[r + 1] = p1 * (d1 - dl);
+            s[r] = p0 * dp[r];
+            s[r + 1] = p1 * dp[r + 1];
           }
         }
         const v8bf b0 = pack_b(s, 0), b1 = pack_b(s, 1);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 0, 0, lane), b0, a0, 0, 0, 0);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 1, 0, lane), b1, a0, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 0), b0, a0, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 0), b1, a0, 0, 0, 0);
         if constexpr (hd > 32) {
-          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 0, 1, lane), b0, a1, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Ki, kb * 32, 1, 1, lane), b1, a1, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 1), b0, a1, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 1), b1, a1, 0, 0, 0);
         }
       }
     };
     if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) body((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max));
     dma_drain();
     __syncthreads();
+  };
+  for (int t = t0; t <= t1; t += 2) {
+    step(std::integral_constant<int, 0>{}, t);
+    if (t + 1 <= t1) step(std::integral_constant<int, 1>{}, t + 1);
   }
+  // dQ = qscale * (dS/dscale . K)
+  const float qscale = DROP ? scale * dscale : scale;
   if (qok) {
     bf16_t* dr = dqkv + (rowbase + myq) * lddq + (long long)hh * hd;
 #pragma unroll
@@ -601,25 +698,21 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
       const int d0 = acc_row(r, lane);
       if (d0 < hd) {
         uint2 w;
-        w.x = (uint32_t)f2bf(a0[r] * scale) | ((uint32_t)f2bf(a0[r + 1] * scale) << 16);
-        w.y = (uint32_t)f2bf(a0[r + 2] * scale) | ((uint32_t)f2bf(a0[r + 3] * scale) << 16);
+        w.x = (uint32_t)f2bf(a0[r] * qscale) | ((uint32_t)f2bf(a0[r + 1] * qscale) << 16);
+        w.y = (uint32_t)f2bf(a0[r + 2] * qscale) | ((uint32_t)f2bf(a0[r + 3] * qscale) << 16);
         *(uint2*)(dr + d0) = w;
       }
       if (d0 + 32 < hd) {
         uint2 w;
-        w.x = (uint32_t)f2bf(a1[r] * scale) | ((uint32_t)f2bf(a1[r + 1] * scale) << 16);
-        w.y = (uint32_t)f2bf(a1[r + 2] * scale) | ((uint32_t)f2bf(a1[r + 3] * scale) << 16);
+        w.x = (uint32_t)f2bf(a1[r] * qscale) | ((uint32_t)f2bf(a1[r + 1] * qscale) << 16);
+        w.y = (uint32_t)f2bf(a1[r + 2] * qscale) | ((uint32_t)f2bf(a1[r + 3] * qscale) << 16);
         *(uint2*)(dr + d0 + 32) = w;
       }
     }
   }
   if (bpart) {  // q-bias gradient partial: column sums of this workgroup's dQ rows (fp32)
-    float* red = (float*)smem;  // the ring is idle after the last barrier
-    colsum_acc(a0, a1, scale, qok, red, 64, 0, wave, lane);
-    __syncthreads();
-    if (tid < hd)
-      bpart[((long long)b * gridDim.y + qtile) * ldp + (long long)hh * hd + tid] =
-          (red[tid] + red[64 + tid]) + (red[128 + tid] + red[192 + tid]);
+    const float v = colsum_wg(a0, a1, qscale, qok, (float*)smem, wave, lane, tid);  // the ring is idle
+    if (tid < hd) bpart[((long long)b * gridDim.y + qtile) * ldp + (long long)hh * hd + tid] = v;
   }
 }
 
@@ -666,6 +759,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     vf[ks] = frag_global(vrow, kok, ks, hd, lane);
   }
   const float c = scale * 1.4426950408889634f;
+  // dS is accumulated divided by the dropout scale (see nd): dK = kscale * (Q^T . dS/dscale)
+  const float ndscale = DROP ? 1.0f / dscale : 1.0f;
+  const float kscale = DROP ? scale * dscale : scale;
   constexpr int nks = (hd + 15) >> 4;
   const uint32_t kcol = ((uint32_t)mykey >> 1) * CG_COLK;
   // the lane's key bit in a pair-split word: key 2c -> bit c, key 2c+1 -> bit 16 + c
@@ -718,7 +814,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       float* fl = (float*)(buf + 2 * IMG);
       int* il = (int*)(buf + 2 * IMG + 2 * 64 * 4);
       fl[tid] = pl * 1.4426950408889634f;
-      fl[64 + tid] = pdl;
+      fl[64 + tid] = -pdl * ndscale;  // nd = -delta / dscale: the dP accumulator's start
       il[tid] = plo;
       il[64 + tid] = DROP == 1 ? (int)cg_row_hash(seed, (uint32_t)(((long long)b * H + h2) * T + q)) : 0;
     }
@@ -731,19 +827,23 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     dma_drain();
   }
   __syncthreads();
-  for (int it = 0; it < total; ++it) {
-    const char* buf = smem + (it & 1) * BUF;
+  const RowOff ro = row_offsets(lane);
+  const TrOff to = tr_offsets(lane);
+  // one iteration on LDS buffer CUR (compile-time: every image read is lane offset + immediate)
+  auto iter = [&](auto cur_c, int it) __attribute__((always_inline)) {
+    constexpr int CUR = decltype(cur_c)::value;
+    const char* buf = smem + CUR * BUF;
     const char* Qi = buf;
     const char* Di = buf + IMG;
     const float* lse2s = (const float*)(buf + 2 * IMG);
-    const float* dls = lse2s + 64;
+    const float* nds = lse2s + 64;
     const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
     const uint32_t* hrs = (const uint32_t*)(buf + 2 * IMG + 3 * 64 * 4);
     const bool more = it + 1 < total;
     // this wave's key word of the tile's keep bits, [query]
     const uint32_t* mws = (const uint32_t*)(buf + 2 * IMG + 4 * 64 * 4) + wave * 64;
     const Cur nx = next_of(cur);
-    if (more) stage_load(nx, (it & 1) ^ 1);  // that buffer was last read before the previous barrier
+    if (more) stage_load(nx, CUR ^ 1);  // that buffer was last read before the previous barrier
     const int q0 = cur.qt * KT;
     // wave activity: some query q in [q0, q0+63] sees some key in [kw0, kw0+31]
     const int qlast = min(T - 1, q0 + KT - 1);
@@ -754,12 +854,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     auto body = [&](bool full) __attribute__((always_inline)) {
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
-        v16f s = zero16(), dp = zero16();
+        // dP starts from -delta/dscale (the rows' nd values): the accumulator then holds
+        // dP - delta/dscale, and dS/dscale = p * (keep ? acc : nd) is one bit-select and a multiply
+        v16f nd;
+#pragma unroll
+        for (int rg = 0; rg < 16; rg += 4) {
+          const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
+          nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
+        }
+        v16f s = zero16(), dp = nd;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           if (ks < nks) {
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Qi, qb * 32, ks, lane), kf[ks], s, 0, 0, 0);
-            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row(Di, qb * 32, ks, lane), vf[ks], dp, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Qi, ro, qb * 32, ks), kf[ks], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
           }
         }
         if (!full) {
@@ -780,9 +888,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         for (int rg = 0; rg < 16; rg += 4) {
           const int qi = qb * 32 + acc_row(rg, lane);  // 4 consecutive queries qi..qi+3
           const float4 l4 = *(const float4*)(lse2s + qi);
-          const float4 d4 = *(const float4*)(dls + qi);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-          const float dv4[4] = {d4.x, d4.y, d4.z, d4.w};
           uint4 hr4 = make_uint4(0, 0, 0, 0);
           if constexpr (DROP == 1) hr4 = *(const uint4*)(hrs + qi);
           uint4 mw4 = make_uint4(0, 0, 0, 0);
@@ -793,44 +899,46 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
           for (int u = 0; u < 4; ++u) {
             const int r = rg + u;
             const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[u]));
-            float d = dp[r];
             float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
             if constexpr (DROP == 1) {
               const uint32_t hsh = cg_pair_mix(hrv[u] + kcol);
               const uint32_t bits = (mykey & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
               const bool keep = bits >= thr;
-              d = keep ? d * dscale : 0.f;
               pdr = keep ? p : 0.f;
-              s[r] = p * (d - dv4[u]);
+              s[r] = p * (keep ? dp[r] : nd[r]);
             } else if constexpr (DROP == 2) {
-              const int m = keep_mask(mwv[u], kpos);
-              pdr = __int_as_float(__float_as_int(p) & m);
-              s[r] = p * fmaf(__int_as_float(__float_as_int(d) & m), dscale, -dv4[u]);
+              const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
+              pdr = __uint_as_float(__float_as_uint(p) & m);
+              s[r] = p * __uint_as_float((__float_as_uint(dp[r]) & m) | (__float_as_uint(nd[r]) & ~m));
             } else {
-              s[r] = p * (d - dv4[u]);
+              s[r] = p * dp[r];
             }
             pd[r] = pdr;
           }
         }
         const v8bf pb0 = pack_b(pd, 0), pb1 = pack_b(pd, 1);
         const v8bf sb0 = pack_b(s, 0), sb1 = pack_b(s, 1);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 0, 0, lane), pb0, dv0, 0, 0, 0);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 1, 0, lane), pb1, dv0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 0, 0, lane), sb0, dk0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 1, 0, lane), sb1, dk0, 0, 0, 0);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 0), pb0, dv0, 0, 0, 0);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 0), pb1, dv0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 0), sb0, dk0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 0), sb1, dk0, 0, 0, 0);
         if constexpr (hd > 32) {
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 0, 1, lane), pb0, dv1, 0, 0, 0);
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Di, qb * 32, 1, 1, lane), pb1, dv1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 0, 1, lane), sb0, dk1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr(Qi, qb * 32, 1, 1, lane), sb1, dk1, 0, 0, 0);
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 1), pb0, dv1, 0, 0, 0);
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 1), pb1, dv1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 1), sb0, dk1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 1), sb1, dk1, 0, 0, 0);
         }
       }
     };
     if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (los[qlast - q0] <= kw0));
-    if (more) stage_store(nx, smem + ((it & 1) ^ 1) * BUF);
+    if (more) stage_store(nx, smem + (CUR ^ 1) * BUF);
     cur = nx;
     dma_drain();
     __syncthreads();
+  };
+  for (int it = 0; it < total; it += 2) {
+    iter(std::integral_constant<int, 0>{}, it);
+    if (it + 1 < total) iter(std::integral_constant<int, 1>{}, it + 1);
   }
   if (kok) {
     bf16_t* kr = dqkv + (rowbase + mykey) * lddq + koff;
@@ -841,8 +949,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       const int d0 = acc_row(r, lane);
       if (d0 < hd) {
         uint2 w;
-        w.x = (uint32_t)f2bf(dk0[r] * scale) | ((uint32_t)f2bf(dk0[r + 1] * scale) << 16);
-        w.y = (uint32_t)f2bf(dk0[r + 2] * scale) | ((uint32_t)f2bf(dk0[r + 3] * scale) << 16);
+        w.x = (uint32_t)f2bf(dk0[r] * kscale) | ((uint32_t)f2bf(dk0[r + 1] * kscale) << 16);
+        w.y = (uint32_t)f2bf(dk0[r + 2] * kscale) | ((uint32_t)f2bf(dk0[r + 3] * kscale) << 16);
         *(uint2*)(kr + d0) = w;
         w.x = (uint32_t)f2bf(dv0[r] * vs) | ((uint32_t)f2bf(dv0[r + 1] * vs) << 16);
         w.y = (uint32_t)f2bf(dv0[r + 2] * vs) | ((uint32_t)f2bf(dv0[r + 3] * vs) << 16);
@@ -850,8 +958,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       }
       if (d0 + 32 < hd) {
         uint2 w;
-        w.x = (uint32_t)f2bf(dk1[r] * scale) | ((uint32_t)f2bf(dk1[r + 1] * scale) << 16);
-        w.y = (uint32_t)f2bf(dk1[r + 2] * scale) | ((uint32_t)f2bf(dk1[r + 3] * scale) << 16);
+        w.x = (uint32_t)f2bf(dk1[r] * kscale) | ((uint32_t)f2bf(dk1[r + 1] * kscale) << 16);
+        w.y = (uint32_t)f2bf(dk1[r + 2] * kscale) | ((uint32_t)f2bf(dk1[r + 3] * kscale) << 16);
         *(uint2*)(kr + d0 + 32) = w;
         w.x = (uint32_t)f2bf(dv1[r] * vs) | ((uint32_t)f2bf(dv1[r + 1] * vs) << 16);
         w.y = (uint32_t)f2bf(dv1[r + 2] * vs) | ((uint32_t)f2bf(dv1[r + 3] * vs) << 16);
@@ -861,13 +969,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   }
   if (bpart) {  // k / v bias gradient partials: column sums of this workgroup's dK, dV rows
     const float vs = DROP ? dscale : 1.0f;
-    float* red = (float*)smem;  // [wave][dK 64 | dV 64]; the ring is idle after the last barrier
-    colsum_acc(dk0, dk1, scale, kok, red, 128, 0, wave, lane);
-    colsum_acc(dv0, dv1, vs, kok, red, 128, 64, wave, lane);
-    __syncthreads();
-    if (tid < 128 && (tid & 63) < hd) {
-      const float v = (red[tid] + red[128 + tid]) + (red[256 + tid] + red[384 + tid]);
-      bpart[((long long)b * gridDim.y + ktile) * ldp + (tid < 64 ? koff + tid : voff + tid - 64)] = v;
+    float* red = (float*)smem;  // the ring is idle after the last barrier
+    const float vk = colsum_wg(dk0, dk1, kscale, kok, red, wave, lane, tid);
+    const float vv = colsum_wg(dv0, dv1, vs, kok, red, wave, lane, tid);
+    float* dst = bpart + ((long long)b * gridDim.y + ktile) * ldp;
+    if (tid < hd) {
+      dst[koff + tid] = vk;
+      dst[voff + tid] = vv;
     }
   }
 }
@@ -885,8 +993,9 @@ static inline size_t attn_drop_mask_words(int B, int T, int H) { return (size_t)
 static inline int attn_drop_mask_launch(uint32_t* mask, int B, int T, int H, uint32_t seed, uint32_t thr,
                                         hipStream_t s) {
   const int nb = cg_cdiv(T, 64);
-  hipLaunchKernelGGL(attn_drop_mask_kernel, dim3(nb * (nb + 1) / 2, B * H), dim3(64), 0, s, mask, T,
-                     attn_drop_wpr(T), seed, thr);
+  const int nbt = nb * (nb + 1) / 2;
+  hipLaunchKernelGGL(attn_drop_mask_kernel, dim3(cg_cdiv(nbt, 4), B * H), dim3(256), 0, s, mask, T,
+                     attn_drop_wpr(T), seed, thr, nbt);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }
@@ -925,9 +1034,11 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   const int wpr = attn_drop_wpr(T);
   const int mode = thr ? (dmask ? 2 : 1) : 0;
   const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
+  // the K/V ring, or the bias-partial reduction buffer when it is larger
+  const size_t shq = bpart ? std::max<size_t>(4 * fa::IMG, fa::COLSUM_LDS) : 4 * fa::IMG;
   cg_probe_begin(CG_PROBE_ATTN_DQ, s);
 #define DQ(D, HDv)                                                                                             \
-  hipLaunchKernelGGL((attn_bwd_dq_mfma<D, HDv>), gq, dim3(256), 4 * fa::IMG, s, qkv, ld, seg, dy, lddy, y, ldy, lse, \
+  hipLaunchKernelGGL((attn_bwd_dq_mfma<D, HDv>), gq, dim3(256), shq, s, qkv, ld, seg, dy, lddy, y, ldy, lse, \
                      delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
 #define DQH(D) if (hd == 64) DQ(D, 64); else if (hd == 48) DQ(D, 48); else DQ(D, 32)
   if (mode == 2) { DQH(2); } else if (mode == 1) { DQH(1); } else { DQH(0); }
@@ -936,7 +1047,8 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_end(CG_PROBE_ATTN_DQ, s, 3.0 * tri);  // S, dP recomputed + dQ
   CG_LAUNCH_CHECK();
   dim3 gk(B * KV, cg_cdiv(T, 128));
-  const size_t shk = 2 * (2 * fa::IMG + 4 * 64 * 4 + (mode == 2 ? 4 * 64 * 4 : 0));
+  const size_t shk = std::max<size_t>(2 * (2 * fa::IMG + 4 * 64 * 4 + (mode == 2 ? 4 * 64 * 4 : 0)),
+                                      bpart ? fa::COLSUM_LDS : 0);
   cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
 #define DKDV(D, HDv)                                                                                            \
   hipLaunchKernelGGL((attn_bwd_dkdv_mfma<D, HDv>), gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv,  \

@@ -211,6 +211,10 @@ struct LayerAct {
 // of qkv (dqkv), all in the compute dtype
 struct DwSlot {
   void *gin, *gattn, *dmlp, *dqkv;
+  // partial rows of the block's parameter / bias gradient column sums, reduced in one batched
+  // launch per dW group (cg_reduce_columns): LayerNorm 2 / 1 backward ([nblk][3d]: dgamma |
+  // dbeta | consumer bias), fc1 bias ([ceil(M/64)][hid]), qkv bias ([B*ceil(T/128)][Nqkv])
+  float *lnp2, *lnp1, *cpart, *bpart;
 };
 struct Acts {
   int32_t* seg;
@@ -281,6 +285,10 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
     sl.gattn = w.take<char>(M * d * es);
     sl.dmlp = w.take<char>(M * (D.swiglu ? 2LL * D.Hp : (long long)D.hid) * es);
     sl.dqkv = w.take<char>(M * D.Nqkv * es);
+    sl.lnp2 = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
+    sl.lnp1 = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
+    sl.cpart = w.take<float>((size_t)((M + 63) / 64) * std::max(D.hid, d) * 4);
+    sl.bpart = w.take<float>((size_t)B * ((T + 127) / 128) * D.Nqkv * 4);
   }
   A.head2 = c->dtype == CG_BF16 ? w.take<char>((size_t)2 * D.Vp * d * 2) : nullptr;
   const long long big = std::max<long long>({(long long)D.hid, 2LL * D.Hp, (long long)D.Nqkv});
@@ -490,6 +498,55 @@ float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 // position of block l inside its dW group (groups run from block L-1 downwards)
 int slot_of(const Dims& D, int l) { return (D.L - 1 - l) % D.G; }
 bool group_ends(const Dims& D, int l) { return l == 0 || slot_of(D, l) == D.G - 1; }
+
+// Parameter / bias gradient reductions deferred to the end of a dW group: the LayerNorm
+// backward and the fused column-sum epilogues of a group's blocks leave partial rows in their
+// slots; one cg_reduce_columns launch per group turns them into gradients (per-layer reduce
+// launches were ~5 us each, mostly idle GPU).  Keyed by model; phase 0 starts a backward.
+std::vector<std::pair<const cg_model*, cg_reduce_batch>>& pending_all() {
+  static std::vector<std::pair<const cg_model*, cg_reduce_batch>> v;
+  return v;
+}
+cg_reduce_batch& pending(const cg_model* m) {
+  auto& v = pending_all();
+  for (auto& e : v)
+    if (e.first == m) return e.second;
+  v.emplace_back(m, cg_reduce_batch{});
+  v.back().second.n = 0;
+  return v.back().second;
+}
+int defer_reduce(const cg_model* m, const float* part, long long ld, int nrows, int cols, float* dst, int accumulate,
+                 void* stream) {
+  cg_reduce_batch& b = pending(m);
+  if (b.n == CG_REDUCE_MAX) {  // full (only with very small groups of very many jobs): drain
+    CK(cg_reduce_columns(&b, stream));
+    b.n = 0;
+  }
+  cg_reduce_job& j = b.j[b.n++];
+  j.part = part; j.ld = ld; j.nrows = nrows; j.cols = cols; j.dst = dst; j.accumulate = accumulate;
+  j.first_block = 0;
+  return CG_OK;
+}
+int flush_reduce(const cg_model* m, void* stream) {
+  cg_reduce_batch& b = pending(m);
+  const int rc = b.n ? cg_reduce_columns(&b, stream) : CG_OK;
+  b.n = 0;
+  return rc;
+}
+// LayerNorm backward whose dgamma / dbeta (/ consumer bias) reductions join the pending batch
+int ln_bwd_deferred(const Ctx& C, int dy_dtype, const void* dy, const float* x, const float* mean, const float* rstd,
+                    long long gw, const float* g_in, void* g_out_t, uint32_t seed, float p, float* part, float* dgamma,
+                    float* dbeta, float* dcol, int accumulate) {
+  const int d = C.D.d;
+  CK(cg_layernorm_bwd_partials(dy_dtype, dy, d, x, d, mean, rstd, P(C, gw), g_in, C.A.g, C.dt, g_out_t, seed, p, part,
+                               dcol ? 1 : 0, (int)C.M, d, C.s));
+  const int nw = dcol ? 3 : 2;
+  const int nblk = cg_layernorm_bwd_blocks((int)C.M);
+  CK(defer_reduce(C.m, part, (long long)nw * d, nblk, d, dgamma, accumulate, C.s));
+  CK(defer_reduce(C.m, part + d, (long long)nw * d, nblk, d, dbeta, accumulate, C.s));
+  if (dcol) CK(defer_reduce(C.m, part + 2 * d, (long long)nw * d, nblk, d, dcol, accumulate, C.s));
+  return CG_OK;
+}
 
 // The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
 // bf16 mode (gemm_dw.h), the per-product GEMMs in fp32 parity mode.
@@ -829,6 +886,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   const uint32_t seed = m->seed;
 
   if (phase == 0) {
+    pending(m).n = 0;  // a backward starts here: drop anything an abandoned one left
     CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
     CK(fill_head2(C, hoff));
@@ -885,9 +943,9 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       // dGELU product; its fused column sums (64-row partials) are fc1's bias gradient
       cg_gemm_desc g = lin_dx(C, sl.gin, d, o.w2, D.hid, d, D.hid, sl.dmlp, D.hid, a.w2T);
       g.epilogue = CG_EPI_DGELU | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
-      g.workspace = A.splitws;
+      g.workspace = sl.cpart;
       CK(cg_gemm(&g, C.s));
-      CK(cg_colsum_reduce(A.splitws, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
+      CK(defer_reduce(m, sl.cpart, D.hid, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
       g = lin_dx(C, sl.dmlp, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
       CK(cg_gemm(&g, C.s));
     } else {
@@ -898,8 +956,8 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(cg_gemm(&g, C.s));
     }
     // gattn = dL/d(proj out); its column sum is the proj bias gradient
-    CK(cg_layernorm_bwd(C.dt, A.dsmall, d, a.xmid, d, a.mean2, a.rstd2, P(C, o.ln2w), A.g, A.g, C.dt, sl.gattn, 0, 0.f,
-                        A.lnpart, G(C, o.ln2w), G(C, o.ln2b), G(C, o.bp), accumulate, (int)M, d, eps, C.s));
+    CK(ln_bwd_deferred(C, C.dt, A.dsmall, a.xmid, a.mean2, a.rstd2, o.ln2w, A.g, sl.gattn, 0, 0.f, sl.lnp2,
+                       G(C, o.ln2w), G(C, o.ln2b), G(C, o.bp), accumulate));
     // ---------------- attention branch
     cg_gemm_desc g = lin_dx(C, sl.gattn, d, o.wp, d, d, d, A.dsmall, d, a.pT);
     CK(cg_gemm(&g, C.s));
@@ -910,7 +968,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     int rc = CG_EUNSUPPORTED;
     if (!D.rope)
       rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
-                       C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, A.bpart, D.Nqkv,
+                       C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, sl.bpart, D.Nqkv,
                        A.delta, C.s);
     const bool fused_bias = rc == CG_OK;
     if (rc == CG_EUNSUPPORTED)
@@ -921,7 +979,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (D.rope)
       CK(cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
     if (fused_bias)
-      CK(cg_colsum_reduce(A.bpart, C.B * ((C.T + 127) / 128), D.Nqkv, G(C, o.bqkv), accumulate, C.s));
+      CK(defer_reduce(m, sl.bpart, D.Nqkv, C.B * ((C.T + 127) / 128), D.Nqkv, G(C, o.bqkv), accumulate, C.s));
     else
       CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
     g = lin_dx(C, sl.dqkv, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
@@ -934,12 +992,16 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // block l-1's MLP output gradient (its bias grad fused as above; it lands in block l-1's
     // gradient range, which is final only after block l-1's group)
     float* db2 = (l > 0 && !D.swiglu) ? G(C, C.Lo.lay[l - 1].b2) : nullptr;
-    CK(cg_layernorm_bwd(C.dt, A.dsmall, d, xl, d, a.mean1, a.rstd1, P(C, o.ln1w), A.g, A.g, C.dt,
-                        l > 0 ? A.slot[slot_of(D, l - 1)].gin : nullptr, site_seed(seed, l - 1, SITE_MLP),
-                        l > 0 ? p : 0.f, A.lnpart, G(C, o.ln1w), G(C, o.ln1b), db2, accumulate, (int)M, d, eps, C.s));
+    CK(ln_bwd_deferred(C, C.dt, A.dsmall, xl, a.mean1, a.rstd1, o.ln1w, A.g,
+                       l > 0 ? A.slot[slot_of(D, l - 1)].gin : nullptr, site_seed(seed, l - 1, SITE_MLP),
+                       l > 0 ? p : 0.f, sl.lnp1, G(C, o.ln1w), G(C, o.ln1b), db2, accumulate));
+    // the group's parameter-gradient reductions (its LayerNorms, fused biases) in one launch,
+    // before the caller starts the group's bucket all-reduce
+    if (group_ends(D, l)) CK(flush_reduce(m, C.s));
     return CG_OK;
   }
   if (phase == 2) {
+    CK(flush_reduce(m, C.s));  // nothing is pending after block 0; kept for partial phase sequences
     // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
     const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
     CK(cg_embed_bwd(m->idx, A.g, G(C, C.Lo.tok), nullptr, C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,

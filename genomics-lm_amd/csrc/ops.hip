@@ -436,17 +436,11 @@ __global__ void ln_param_reduce_kernel(const float* __restrict__ partials, int n
   *dst = accumulate ? *dst + s : s;
 }
 
-extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
-                                const float* mean, const float* rstd, const float* gamma, const float* g_in,
-                                float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
-                                float* partials, float* dgamma, float* dbeta, float* dcolsum, int accumulate,
-                                int rows, int cols, float eps, void* stream) {
-  (void)eps;
-  if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
-  if (dcolsum && (!g_out_t || !dgamma || !dbeta)) return CG_EINVAL;
-  const int want_col = dcolsum ? 1 : 0;
-  if (rows <= 0) return CG_OK;
-  hipStream_t s = (hipStream_t)stream;
+// the row pass (g_out, g_out_t, per-block partial rows); *fast: the vectorised kernel ran
+static int ln_bwd_rows(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx, const float* mean,
+                       const float* rstd, const float* gamma, const float* g_in, float* g_out, int out_dtype,
+                       void* g_out_t, uint32_t drop_seed, float drop_p, float* partials, int want_col, int rows,
+                       int cols, hipStream_t s, bool* fast_out) {
   const int nblk = cg_layernorm_bwd_blocks(rows);
   const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   const float dscale = drop_p > 0.f ? 1.0f / (1.0f - drop_p) : 1.0f;
@@ -469,30 +463,118 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
                                              g_out, (float*)g_out_t, drop_seed, thr, dscale, partials, rows, want_col);
     }
   }
-  if (fast) {
-    CG_LAUNCH_CHECK();
-    if (dgamma && dbeta) {
-      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 16)), dim3(1024), 0, s, partials, nblk,
-                         cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
-      CG_LAUNCH_CHECK();
-    }
-    return CG_OK;
-  }
+  if (!fast) {
 #define LNB(TD, TO)                                                                                  \
   hipLaunchKernelGGL((ln_bwd_kernel<TD, TO>), dim3(nblk), dim3(256), 0, s, (const TD*)dy, lddy, x, ldx, \
                      mean, rstd, gamma, g_in, g_out, (TO*)g_out_t, drop_seed, thr, dscale, partials, rows, cols, want_col)
-  if (dy_dtype == CG_BF16) {
-    if (out_dtype == CG_BF16) LNB(bf16_t, bf16_t); else LNB(bf16_t, float);
-  } else {
-    if (out_dtype == CG_BF16) LNB(float, bf16_t); else LNB(float, float);
-  }
+    if (dy_dtype == CG_BF16) {
+      if (out_dtype == CG_BF16) LNB(bf16_t, bf16_t); else LNB(bf16_t, float);
+    } else {
+      if (out_dtype == CG_BF16) LNB(float, bf16_t); else LNB(float, float);
+    }
 #undef LNB
+  }
   CG_LAUNCH_CHECK();
+  *fast_out = fast;
+  return CG_OK;
+}
+
+extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
+                                const float* mean, const float* rstd, const float* gamma, const float* g_in,
+                                float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
+                                float* partials, float* dgamma, float* dbeta, float* dcolsum, int accumulate,
+                                int rows, int cols, float eps, void* stream) {
+  (void)eps;
+  if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
+  if (dcolsum && (!g_out_t || !dgamma || !dbeta)) return CG_EINVAL;
+  const int want_col = dcolsum ? 1 : 0;
+  if (rows <= 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = cg_layernorm_bwd_blocks(rows);
+  bool fast = false;
+  const int rc = ln_bwd_rows(dy_dtype, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, out_dtype, g_out_t, drop_seed,
+                             drop_p, partials, want_col, rows, cols, s, &fast);
+  if (rc != CG_OK) return rc;
   if (dgamma && dbeta) {
-    hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cg_cdiv((2 + want_col) * cols, 256)), dim3(256), 0, s, partials,
-                       nblk, cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
+    if (fast)
+      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 16)), dim3(1024), 0, s, partials, nblk,
+                         cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
+    else
+      hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cg_cdiv((2 + want_col) * cols, 256)), dim3(256), 0, s, partials,
+                         nblk, cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
     CG_LAUNCH_CHECK();
   }
+  return CG_OK;
+}
+
+extern "C" int cg_layernorm_bwd_partials(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
+                                         const float* mean, const float* rstd, const float* gamma, const float* g_in,
+                                         float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
+                                         float* partials, int want_col, int rows, int cols, void* stream) {
+  if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
+  if (!partials || (want_col && !g_out_t)) return CG_EINVAL;
+  if (rows <= 0) return CG_OK;
+  bool fast = false;
+  return ln_bwd_rows(dy_dtype, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, out_dtype, g_out_t, drop_seed, drop_p,
+                     partials, want_col ? 1 : 0, rows, cols, (hipStream_t)stream, &fast);
+}
+
+// Batched column reductions (cg_reduce_columns): one 1024-thread block = 16 columns x 64 row
+// lanes of one job, 4 independent chains per lane, the same fixed order as ln_param_reduce2 (so a
+// deferred LayerNorm reduction is bitwise the in-call one); the block finds its job by a scan
+// over the (<= CG_REDUCE_MAX) first-block offsets
+__global__ __launch_bounds__(1024) void reduce_columns_kernel(cg_reduce_batch bt) {
+  __shared__ float red[64][17];
+  int j = 0;
+  while (j + 1 < bt.n && bt.j[j + 1].first_block <= (int)blockIdx.x) ++j;
+  const cg_reduce_job& jb = bt.j[j];
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  const int c = ((int)blockIdx.x - jb.first_block) * 16 + tx;
+  float s = 0.f;
+  if (c < jb.cols) {
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    int b = ty;
+    for (; b + 192 < jb.nrows; b += 256)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s4[u] += jb.part[(long long)(b + 64 * u) * jb.ld + c];
+    for (; b < jb.nrows; b += 64) s4[0] += jb.part[(long long)b * jb.ld + c];
+    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  }
+  red[ty][tx] = s;
+  __syncthreads();
+  float v = 0.f;
+  if (ty < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v += red[ty * 8 + i][tx];
+  }
+  __syncthreads();
+  if (ty < 8) red[ty][tx] = v;
+  __syncthreads();
+  if (ty == 0 && c < jb.cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][tx];
+    jb.dst[c] = jb.accumulate ? jb.dst[c] + t : t;
+  }
+}
+
+extern "C" int cg_reduce_columns(const cg_reduce_batch* batch, void* stream) {
+  if (!batch || batch->n < 0 || batch->n > CG_REDUCE_MAX) return CG_EINVAL;
+  cg_reduce_batch bt = *batch;
+  int nb = 0, k = 0;
+  for (int i = 0; i < batch->n; ++i) {
+    const cg_reduce_job& q = batch->j[i];
+    if (q.cols < 0 || q.nrows < 0 || ((!q.part || !q.dst) && q.cols > 0)) return CG_EINVAL;
+    if (q.cols == 0) continue;
+    bt.j[k] = q;
+    bt.j[k].first_block = nb;
+    nb += cg_cdiv(q.cols, 16);
+    ++k;
+  }
+  bt.n = k;
+  if (nb == 0) return CG_OK;
+  hipLaunchKernelGGL(reduce_columns_kernel, dim3(nb), dim3(1024), 0, (hipStream_t)stream, bt);
+  CG_LAUNCH_CHECK();
   return CG_OK;
 }
 

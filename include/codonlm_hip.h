@@ -111,6 +111,33 @@ int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* 
                      uint32_t drop_seed, float drop_p, float* partials, float* dgamma,
                      float* dbeta, float* dcolsum, int accumulate, int rows, int cols, float eps,
                      void* stream);
+/* the same backward without the reduction: only the partial rows are written,
+ * [nblk][(2 + want_col) * cols] = dgamma | dbeta | (consumer column sums); they are reduced
+ * later, batched with other layers' partials, by cg_reduce_columns (the engine defers the
+ * per-layer parameter-gradient reductions of a dW group to one launch) */
+int cg_layernorm_bwd_partials(int dy_dtype, const void* dy, long long lddy, const float* x,
+                              long long ldx, const float* mean, const float* rstd,
+                              const float* gamma, const float* g_in, float* g_out, int out_dtype,
+                              void* g_out_t, uint32_t drop_seed, float drop_p, float* partials,
+                              int want_col, int rows, int cols, void* stream);
+
+/* batched column reductions of partial rows (parameter / bias gradients, the backward of the
+ * sums autograd performs per nn.Parameter): per job, dst[c] (+)= sum_r part[r * ld + c],
+ * c < cols, r < nrows, in a fixed summation order; all jobs in one launch */
+typedef struct {
+  const float* part;
+  long long ld;
+  int nrows, cols;
+  float* dst;
+  int accumulate;
+  int first_block; /* filled by cg_reduce_columns */
+} cg_reduce_job;
+#define CG_REDUCE_MAX 48
+typedef struct {
+  int n;
+  cg_reduce_job j[CG_REDUCE_MAX];
+} cg_reduce_batch;
+int cg_reduce_columns(const cg_reduce_batch* batch, void* stream);
 
 /* token + position embedding (+dropout) -- model_tiny_gpt.py:305-312 */
 int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const float* pos_emb, float* x,

@@ -121,6 +121,44 @@ def test_layernorm_fwd_bwd(out_dtype, cols):
     assert (csum.cpu() - exp_t.sum(0)).abs().max() < 2e-3
 
 
+@pytest.mark.parametrize("cols", [512, 100])
+def test_layernorm_bwd_partials_deferred_reduce(cols):
+    """The engine's deferred path (row pass writing partials + one batched cg_reduce_columns over
+    several layers' partials) gives bitwise the in-call reduction of cg_layernorm_bwd."""
+    ops = _ops()
+    rows = 4096 + 37
+    g = torch.Generator().manual_seed(11 + cols)
+    x = (torch.randn(rows, cols, generator=g) * 2 + 0.5).to(DEV)
+    w = (1 + 0.1 * torch.randn(cols, generator=g)).to(DEV)
+    b = (0.1 * torch.randn(cols, generator=g)).to(DEV)
+    _, mean, rstd = ops.layernorm_fwd(x, w, b, out_dtype=torch.bfloat16)
+    dy = torch.randn(rows, cols, generator=g).to(DEV).to(torch.bfloat16)
+    gin = torch.randn(rows, cols, generator=g).to(DEV)
+    go, dgam, dbet, br_t, csum = ops.layernorm_bwd(dy, x, mean, rstd, w, g_in=gin, branch_dtype=torch.bfloat16,
+                                                   drop_seed=5, drop_p=0.1)
+    go_p, part, br_p = ops.layernorm_bwd_partials(dy, x, mean, rstd, w, g_in=gin, branch_dtype=torch.bfloat16,
+                                                  drop_seed=5, drop_p=0.1)
+    assert torch.equal(go_p, go) and torch.equal(br_p, br_t)
+    # a second, unrelated job in the same batch (accumulating) and a 2-wide LayerNorm job
+    other = torch.randn(96, 2048, generator=g).to(DEV)
+    acc0 = torch.randn(2048, generator=g).to(DEV)
+    acc = acc0.clone()
+    outs = [torch.full((cols,), float("nan"), device=DEV) for _ in range(3)]
+    ops.reduce_columns([(part[:, :cols], outs[0], 0), (other, acc, 1), (part[:, cols:2 * cols], outs[1], 0),
+                        (part[:, 2 * cols:], outs[2], 0)])
+    torch.cuda.synchronize()
+    # bitwise where the vectorised row pass ran (its in-call reduction has the batched kernel's order)
+    same = torch.equal if cols % 128 == 0 else (lambda a, e: (a - e).abs().max().item() <= 1e-4 * (1 + e.abs().max().item()))
+    assert same(outs[0], dgam) and same(outs[1], dbet) and same(outs[2], csum)
+    ref = acc0.double() + other.double().sum(0)
+    assert (acc.double() - ref).abs().max().item() < 1e-4
+    _, part2, _ = ops.layernorm_bwd_partials(dy, x, mean, rstd, w)
+    assert part2.shape[1] == 2 * cols
+    d2 = torch.empty(cols, device=DEV)
+    ops.reduce_columns([(part2[:, :cols], d2, 0)])
+    assert same(d2, dgam)
+
+
 def test_segment_starts():
     ops = _ops()
     idx = torch.randint(4, 68, (3, 700))
