@@ -209,6 +209,14 @@ __device__ __forceinline__ v8bf keep_b(v8bf u, int s, uint32_t w) {
   for (int i = 0; i < 4; ++i) v[i] = keep_pk(v[i], w, kbit(8 * s + 2 * i));
   return __builtin_bit_cast(v8bf, v);
 }
+// a register fragment times c, rounded to bf16 once (S = (cQ)K^T or Q(cK)^T lands in the exp2
+// domain: the backward's p = exp2(S - lse2) then needs no multiply)
+__device__ __forceinline__ v8bf scale_frag(v8bf f, float c) {
+  v8bf r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)((float)f[j] * c);
+  return r;
+}
 // A operand of all ones: ones x B sums B over its k rows into every row of the result
 __device__ __forceinline__ v8bf ones_frag() {
   v8bf o;
@@ -602,20 +610,26 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
   // dP starts from nd = -delta/dscale, added by one MFMA (ones x [hi; lo] split-bf16 nd rows:
   // exact to ~2^-16): the accumulator is dP - delta/dscale and dS/dscale = p * (keep ? acc : nd)
   const float nd = -dl * (DROP ? 1.0f / dscale : 1.0f);
-  v8bf ndfrag, onesk;
+  // likewise S starts from -lse2 with Q pre-multiplied by c = scale*log2(e): the accumulator is
+  // then the exp2 argument itself
+  v8bf ndfrag, lsefrag, onesk;
   {
-    const __bf16 hi = (__bf16)nd;
-    const __bf16 lo = (__bf16)(nd - (float)hi);
+    const __bf16 hi = (__bf16)nd, lhi = (__bf16)(-lse2);
+    const __bf16 lo = (__bf16)(nd - (float)hi), llo = (__bf16)(-lse2 - (float)lhi);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       ndfrag[j] = (__bf16)0.f;
+      lsefrag[j] = (__bf16)0.f;
       onesk[j] = (__bf16)0.f;
     }
     if (lane < 32) {
       ndfrag[0] = hi; ndfrag[1] = lo;
+      lsefrag[0] = lhi; lsefrag[1] = llo;
       onesk[0] = (__bf16)1.f; onesk[1] = (__bf16)1.f;
     }
   }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) qf[ks] = scale_frag(qf[ks], c);
   auto step = [&](auto cur_c, int t) __attribute__((always_inline)) {
     constexpr int CUR = decltype(cur_c)::value;
     const char* Ki = smem + CUR * 2 * IMG;
@@ -635,7 +649,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
     auto body = [&](bool full) __attribute__((always_inline)) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        v16f s = zero16();
+        v16f s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, lsefrag, zero16(), 0, 0, 0);
         v16f dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, ndfrag, zero16(), 0, 0, 0);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
@@ -656,8 +670,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
         const uint32_t wb = (kb ? wc.y : wc.x) >> (2 * (lane >> 5));
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          const float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lse2));
-          const float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], c, -lse2));
+          const float p0 = __builtin_amdgcn_exp2f(s[r]);
+          const float p1 = __builtin_amdgcn_exp2f(s[r + 1]);
           if constexpr (DROP == 1) {
             const uint32_t off = (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2));
             const uint32_t hsh = cg_pair_mix(hb + off * CG_COLK);
@@ -752,13 +766,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   const long long voff = (long long)(H + KV) * hd + (long long)kvh * hd;
   const bf16_t* krow = qkv + (rowbase + (kok ? mykey : 0)) * ld + koff;
   const bf16_t* vrow = qkv + (rowbase + (kok ? mykey : 0)) * ld + voff;
+  const float c = scale * 1.4426950408889634f;  // K is pre-multiplied by it (exp2 domain)
   v8bf kf[4], vf[4];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    kf[ks] = frag_global(krow, kok, ks, hd, lane);
+    kf[ks] = scale_frag(frag_global(krow, kok, ks, hd, lane), c);
     vf[ks] = frag_global(vrow, kok, ks, hd, lane);
   }
-  const float c = scale * 1.4426950408889634f;
   // dS is accumulated divided by the dropout scale (see nd): dK = kscale * (Q^T . dS/dscale)
   const float ndscale = DROP ? 1.0f / dscale : 1.0f;
   const float kscale = DROP ? scale * dscale : scale;
@@ -813,7 +827,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       const int q = qt * KT + tid;
       float* fl = (float*)(buf + 2 * IMG);
       int* il = (int*)(buf + 2 * IMG + 2 * 64 * 4);
-      fl[tid] = pl * 1.4426950408889634f;
+      fl[tid] = -pl * 1.4426950408889634f;  // -lse2: the S accumulator's start
       fl[64 + tid] = -pdl * ndscale;  // nd = -delta / dscale: the dP accumulator's start
       il[tid] = plo;
       il[64 + tid] = DROP == 1 ? (int)cg_row_hash(seed, (uint32_t)(((long long)b * H + h2) * T + q)) : 0;
@@ -856,13 +870,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       for (int qb = 0; qb < 2; ++qb) {
         // dP starts from -delta/dscale (the rows' nd values): the accumulator then holds
         // dP - delta/dscale, and dS/dscale = p * (keep ? acc : nd) is one bit-select and a multiply
-        v16f nd;
+        // S starts from -lse2 (K is pre-multiplied by c = scale*log2(e)): the accumulator is the
+        // exp2 argument itself
+        v16f nd, s;
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 4) {
           const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
           nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
+          const float4 l4 = *(const float4*)(lse2s + qb * 32 + acc_row(rg, lane));
+          s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
         }
-        v16f s = zero16(), dp = nd;
+        v16f dp = nd;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           if (ks < nks) {
@@ -887,8 +905,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 4) {
           const int qi = qb * 32 + acc_row(rg, lane);  // 4 consecutive queries qi..qi+3
-          const float4 l4 = *(const float4*)(lse2s + qi);
-          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
           uint4 hr4 = make_uint4(0, 0, 0, 0);
           if constexpr (DROP == 1) hr4 = *(const uint4*)(hrs + qi);
           uint4 mw4 = make_uint4(0, 0, 0, 0);
@@ -898,7 +914,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int r = rg + u;
-            const float p = __builtin_amdgcn_exp2f(fmaf(s[r], c, -lv[u]));
+            const float p = __builtin_amdgcn_exp2f(s[r]);
             float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
             if constexpr (DROP == 1) {
               const uint32_t hsh = cg_pair_mix(hrv[u] + kcol);

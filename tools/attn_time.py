@@ -66,7 +66,7 @@ def main():
 
         res = {"lib": str(path)}
         for name, fn in (("mask", msk), ("fwd", fwd), ("bwd_bias", lambda: bwd(bpart)), ("bwd", lambda: bwd(None))):
-            for _ in range(3):
+            for _ in range(10):
                 fn()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
