@@ -143,6 +143,31 @@ def reduce_columns(jobs):
             "cg_reduce_columns")
 
 
+def swiglu_fwd(gu, H):
+    """s[:, j] = silu(gu[:, j]) * gu[:, Hp + j] for j < H (0 for H <= j < Hp), Hp = gu.shape[1] // 2."""
+    rows, Hp = gu.shape[0], gu.shape[1] // 2
+    s = torch.empty(rows, Hp, dtype=gu.dtype, device=gu.device)
+    L.check(L.lib.cg_swiglu_fwd(_dt(gu), gu.data_ptr(), gu.stride(0), Hp, s.data_ptr(), s.stride(0), rows, H,
+                                L.stream_ptr(gu.device)), "cg_swiglu_fwd")
+    return s
+
+
+def swiglu_bwd(gu, ds, H):
+    """d(gate | up) of swiglu_fwd for the upstream gradient ds [rows][Hp]."""
+    rows, Hp = gu.shape[0], gu.shape[1] // 2
+    dgu = torch.empty_like(gu)
+    L.check(L.lib.cg_swiglu_bwd(_dt(gu), gu.data_ptr(), gu.stride(0), Hp, ds.data_ptr(), ds.stride(0),
+                                dgu.data_ptr(), dgu.stride(0), rows, H, L.stream_ptr(gu.device)), "cg_swiglu_bwd")
+    return dgu
+
+
+def rope_(qkv, B, T, H, KV, hd, cos_tab, sin_tab, inverse=False):
+    """In-place rotate-half RoPE of the q and k heads of qkv [B*T][ld] (cos/sin fp32 [T][hd/2])."""
+    L.check(L.lib.cg_rope_tab(_dt(qkv), qkv.data_ptr(), qkv.stride(0), B, T, H, KV, hd, cos_tab.data_ptr(),
+                              sin_tab.data_ptr(), int(inverse), L.stream_ptr(qkv.device)), "cg_rope_tab")
+    return qkv
+
+
 def segment_starts(idx, sep_id):
     B, T = idx.shape
     out = torch.empty(B, T, dtype=torch.int32, device=idx.device)

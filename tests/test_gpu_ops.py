@@ -159,6 +159,63 @@ def test_layernorm_bwd_partials_deferred_reduce(cols):
     assert same(d2, dgam)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H,Hp,ld_pad", [(1024, 1024, 0), (1365, 1408, 0), (100, 104, 8), (50, 51, 0)])
+def test_swiglu_fwd_bwd(dtype, H, Hp, ld_pad):
+    """model_tiny_gpt.py:47-57: vectorised 8-element runs (Hp % 8 == 0, aligned rows) and the scalar
+    fallback (odd Hp), against torch autograd of silu(g) * u."""
+    ops = _ops()
+    rows = 333
+    g = torch.Generator().manual_seed(H)
+    full = torch.randn(rows, 2 * Hp + ld_pad, generator=g) * 2
+    gu = full.to(DEV, dtype)[:, :2 * Hp]
+    ds = torch.randn(rows, Hp, generator=g).to(DEV, dtype)
+    s = ops.swiglu_fwd(gu, H)
+    dgu = ops.swiglu_bwd(gu, ds, H)
+    gr = gu.float().cpu()[:, :H].clone().requires_grad_(True)
+    ur = gu.float().cpu()[:, Hp:Hp + H].clone().requires_grad_(True)
+    ref = F.silu(gr) * ur
+    ref.backward(ds.float().cpu()[:, :H])
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    sc = s.float().cpu()
+    assert (sc[:, :H] - ref.detach()).abs().max() <= tol * (1 + ref.abs().max())
+    assert torch.all(sc[:, H:] == 0)
+    d = dgu.float().cpu()
+    assert (d[:, :H] - gr.grad).abs().max() <= tol * (1 + gr.grad.abs().max())
+    assert (d[:, Hp:Hp + H] - ur.grad).abs().max() <= tol * (1 + ur.grad.abs().max())
+    assert torch.all(d[:, H:Hp] == 0) and torch.all(d[:, Hp + H:] == 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H,KV,hd", [(8, 4, 48), (4, 4, 64), (2, 1, 20)])
+def test_rope_forward_inverse(dtype, H, KV, hd):
+    """model_tiny_gpt.py:9-45 rotate-half RoPE on the q and k heads (v untouched); inverse undoes it.
+    hd 48 / 64 take the vectorised path, hd 20 (half = 10) the scalar one."""
+    ops = _ops()
+    B, T = 3, 77
+    ld = (H + 2 * KV) * hd
+    g = torch.Generator().manual_seed(hd)
+    qkv0 = torch.randn(B * T, ld, generator=g)
+    half = hd // 2
+    inv = 1.0 / (10000 ** (torch.arange(half, dtype=torch.float64) / half))
+    ang = torch.arange(T, dtype=torch.float64)[:, None] * inv[None, :]
+    cos, sin = torch.cos(ang).float(), torch.sin(ang).float()
+    x = qkv0.to(DEV, dtype)
+    ops.rope_(x, B, T, H, KV, hd, cos.to(DEV), sin.to(DEV))
+    xr = x.float().cpu().view(B, T, -1)
+    src = qkv0.to(dtype).float().view(B, T, -1)
+    for h in range(H + KV):
+        a = src[..., h * hd:h * hd + half]
+        b = src[..., h * hd + half:(h + 1) * hd]
+        exp = torch.cat([a * cos - b * sin, b * cos + a * sin], -1)
+        tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+        assert (xr[..., h * hd:(h + 1) * hd] - exp).abs().max() <= tol * 4
+    assert torch.equal(xr[..., (H + KV) * hd:], src[..., (H + KV) * hd:])
+    ops.rope_(x, B, T, H, KV, hd, cos.to(DEV), sin.to(DEV), inverse=True)
+    tol = 3e-2 if dtype == torch.bfloat16 else 1e-5
+    assert (x.float().cpu() - qkv0.to(dtype).float()).abs().max() <= tol * 4
+
+
 def test_segment_starts():
     ops = _ops()
     idx = torch.randint(4, 68, (3, 700))
