@@ -28,7 +28,7 @@ def _p(t):
 
 def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=None, out_dtype=None,
          bias=None, resid=None, epilogue=0, aux=None, aux_out=None, alpha=1.0, drop_seed=0, drop_p=0.0,
-         split_k=1, colsum_out=None):
+         split_k=1, colsum_out=None, n_valid=0):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); A(m,k)=a[m,k] if a_kcontig else a[k,m]; same for B.
     colsum_out (fp32 [N]): also the column sums of C (CG_EPI_COLSUM partials + cg_colsum_reduce)."""
     for t in (a, b):
@@ -68,6 +68,7 @@ def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=No
     d.ld_aux = aux_t.stride(0) if aux_t is not None else 0
     d.drop_seed, d.drop_p = int(drop_seed) & 0xFFFFFFFF, float(drop_p)
     d.split_k, d.workspace = int(split_k), _p(ws)
+    d.n_valid = int(n_valid)
     L.check(L.lib.cg_gemm(C.byref(d), L.stream_ptr(a.device)), "cg_gemm")
     if colsum_out is not None:
         L.check(L.lib.cg_colsum_reduce(ws.data_ptr(), (M + 63) // 64, N, colsum_out.data_ptr(), 0,

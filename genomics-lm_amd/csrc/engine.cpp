@@ -808,9 +808,17 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
       g.drop_seed = site_seed(seed, l, SITE_MLP); g.drop_p = p;
       CK(cg_gemm(&g, C.s));
     } else {
-      g = lin_fwd(C, a.h2, d, o.wgu, d, 2 * D.Hp, d, a.gu, 2 * D.Hp);
-      CK(cg_gemm(&g, C.s));
-      CK(cg_swiglu_fwd(C.dt, a.gu, 2 * D.Hp, D.Hp, a.s, D.Hp, (int)M, D.hid, C.s));
+      // gate|up product with SwiGLU in its epilogue (s to a.s, pre-activations to a.gu); the
+      // separate pass where the fused tile does not apply (fp32, unaligned shapes)
+      g = lin_fwd(C, a.h2, d, o.wgu, d, D.Hp, d, a.s, D.Hp);
+      g.epilogue = CG_EPI_SWIGLU; g.aux_out = a.gu; g.ld_aux = 2 * D.Hp; g.n_valid = D.hid;
+      int rc = C.dt == CG_BF16 ? cg_gemm(&g, C.s) : CG_EUNSUPPORTED;
+      if (rc == CG_EUNSUPPORTED) {
+        g = lin_fwd(C, a.h2, d, o.wgu, d, 2 * D.Hp, d, a.gu, 2 * D.Hp);
+        CK(cg_gemm(&g, C.s));
+        rc = cg_swiglu_fwd(C.dt, a.gu, 2 * D.Hp, D.Hp, a.s, D.Hp, (int)M, D.hid, C.s);
+      }
+      CK(rc);
       g = lin_fwd(C, a.s, D.Hp, o.wd, D.Hp, d, D.Hp, xn, d);
       g.c_dtype = CG_F32;
       g.epilogue = CG_EPI_RESID | (p > 0 ? CG_EPI_DROPOUT : 0);
@@ -949,9 +957,16 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       g = lin_dx(C, sl.dmlp, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
       CK(cg_gemm(&g, C.s));
     } else {
-      cg_gemm_desc g = lin_dx(C, sl.gin, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp, a.wdT);
-      CK(cg_gemm(&g, C.s));
-      CK(cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, sl.dmlp, 2 * D.Hp, (int)M, D.hid, C.s));
+      // dL/ds product with the SwiGLU backward in its epilogue (d(gate|up) straight to dmlp)
+      cg_gemm_desc g = lin_dx(C, sl.gin, d, o.wd, D.Hp, d, D.Hp, sl.dmlp, 2 * D.Hp, a.wdT);
+      g.epilogue = CG_EPI_DSWIGLU; g.aux = a.gu; g.ld_aux = 2 * D.Hp; g.n_valid = D.hid;
+      int rc = C.dt == CG_BF16 ? cg_gemm(&g, C.s) : CG_EUNSUPPORTED;
+      if (rc == CG_EUNSUPPORTED) {
+        g = lin_dx(C, sl.gin, d, o.wd, D.Hp, d, D.Hp, A.dsmall, D.Hp, a.wdT);
+        CK(cg_gemm(&g, C.s));
+        rc = cg_swiglu_bwd(C.dt, a.gu, 2 * D.Hp, D.Hp, A.dsmall, D.Hp, sl.dmlp, 2 * D.Hp, (int)M, D.hid, C.s);
+      }
+      CK(rc);
       g = lin_dx(C, sl.dmlp, 2 * D.Hp, o.wgu, d, 2 * D.Hp, d, A.dsmall, d, a.wguT);
       CK(cg_gemm(&g, C.s));
     }

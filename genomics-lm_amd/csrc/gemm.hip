@@ -25,6 +25,7 @@ struct GemmParams {
   const void* aux; void* aux_out; long long ld_aux;
   uint32_t drop_seed, drop_thr; float drop_scale;
   float* ws; int split;
+  int n_valid;  // SWIGLU / DSWIGLU live columns
 };
 
 // ---------------------------------------------------------------------------
@@ -516,6 +517,8 @@ static gemm_kernel_t pick_pers(int e, int ct) {
   PSPEC(CG_EPI_ACCUM, CG_F32)
   PSPEC(CG_EPI_DGELU | CG_EPI_COLSUM, CG_BF16)
   PSPEC(CG_EPI_COLSUM, CG_BF16)
+  PSPEC(CG_EPI_SWIGLU, CG_BF16)
+  PSPEC(CG_EPI_DSWIGLU, CG_BF16)
 #undef PSPEC
   return nullptr;
 }
@@ -553,6 +556,12 @@ static bool use_pers(const cg_gemm_desc* d, int split) {
   if (((long long)(d->M - 1) * d->ldc + d->N) * es >= lim) return false;
   if ((d->epilogue & CG_EPI_RESID) && ((long long)(d->M - 1) * d->ldr + d->N) * 4 >= lim) return false;
   if ((d->epilogue & (CG_EPI_GELU | CG_EPI_DGELU)) && ((long long)(d->M - 1) * d->ld_aux + d->N) * es >= lim)
+    return false;
+  // SwiGLU: B has 2N rows; aux / aux_out (and C for DSWIGLU) are 2N columns wide
+  if ((d->epilogue & (CG_EPI_SWIGLU | CG_EPI_DSWIGLU)) &&
+      (((long long)(2 * d->N - 1) * d->ldb + d->K) * 2 >= lim ||
+       ((long long)(d->M - 1) * d->ld_aux + 2 * d->N) * 2 >= lim ||
+       ((long long)(d->M - 1) * d->ldc + 2 * d->N) * 2 >= lim))
     return false;
   return true;
 }
@@ -612,6 +621,18 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   if ((p.epi & CG_EPI_GELU) && !p.aux_out) return CG_EINVAL;
   if ((p.epi & CG_EPI_DGELU) && !p.aux) return CG_EINVAL;
   if ((p.epi & CG_EPI_COLSUM) && (!d->workspace || d->split_k > 1)) return CG_EINVAL;
+  // SwiGLU epilogues: only the persistent bf16 tile implements them (the caller keeps the
+  // separate cg_swiglu_* passes on CG_EUNSUPPORTED)
+  const bool swg = (p.epi & (CG_EPI_SWIGLU | CG_EPI_DSWIGLU)) != 0;
+  if (swg) {
+    if (p.epi != CG_EPI_SWIGLU && p.epi != CG_EPI_DSWIGLU) return CG_EUNSUPPORTED;
+    if (d->in_dtype != CG_BF16 || p.c_dtype != CG_BF16 || d->split_k > 1 || !d->a_kcontig || !d->b_kcontig ||
+        p.alpha != 1.0f || (p.N & 63) || (p.ldc & 7) || (p.ld_aux & 7) || ((uintptr_t)p.C & 15) ||
+        ((uintptr_t)(p.epi == CG_EPI_SWIGLU ? p.aux_out : p.aux) & 15))
+      return CG_EUNSUPPORTED;
+    if (p.epi == CG_EPI_SWIGLU ? !p.aux_out : !p.aux) return CG_EINVAL;
+    p.n_valid = d->n_valid > 0 ? std::min(d->n_valid, p.N) : p.N;
+  }
   int split = d->split_k > 1 ? d->split_k : 1;
   const int bkt = d->in_dtype == CG_BF16 ? bfg::BKT : 16;
   if (d->K == 0) split = 1;
@@ -639,12 +660,13 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     vec = vec_ok(d, split);
     gemm_kernel_t k;
     const bool pers = vec && use_pers(d, split);
+    if (swg && !pers) return CG_EUNSUPPORTED;
     if (!pers) p.epi &= ~CG_EPI_COLSUM;  // only the persistent tile fuses the column sums
     const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
     if (pers) {
       k = pick_pers(p.epi, p.c_dtype);
       colsum_fused = colsum;
-      const int tiles = cg_cdiv(p.N, bfp::BN) * cg_cdiv(p.M, bfp::BM);
+      const int tiles = cg_cdiv(p.N, (p.epi & CG_EPI_SWIGLU) ? bfp::BN / 2 : bfp::BN) * cg_cdiv(p.M, bfp::BM);
       g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cu_count()));
       blk = dim3(bfp::THREADS);
       sh = bfp::SMEM;

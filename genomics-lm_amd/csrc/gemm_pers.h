@@ -51,13 +51,23 @@ __device__ __forceinline__ v8bf bfrag(const char* img, int wn, int j, int ks, in
 template <int EPI, int CT>
 struct Epi {
   static constexpr int W = CT == CG_BF16 ? 1 : 2;  // 16-B accesses per 8 values of C dtype
-  // epilogue operand LOADS (bias, residual, dGELU pre-activation, accumulate source), issued
-  // at the top of the tile's last k-step, before that step's DMAs
-  static constexpr int L = 8 * (((EPI & CG_EPI_RESID) ? 2 : 0) + ((EPI & CG_EPI_DGELU) ? W : 0) +
-                                ((EPI & CG_EPI_ACCUM) ? 2 : 0)) + ((EPI & CG_EPI_BIAS) ? 4 : 0);
-  // epilogue STORES (C, GELU pre-activation, column-sum partials), issued after the last k-step
-  static constexpr int S = 8 * (W + ((EPI & CG_EPI_GELU) ? W : 0)) + ((EPI & CG_EPI_COLSUM) ? 4 : 0);
+  static constexpr bool SWG = EPI == CG_EPI_SWIGLU, DSW = EPI == CG_EPI_DSWIGLU;
+  // epilogue operand LOADS (bias, residual, dGELU pre-activation, accumulate source, SwiGLU
+  // gate|up), issued at the top of the tile's last k-step, before that step's DMAs
+  static constexpr int L = DSW ? 16
+                               : 8 * (((EPI & CG_EPI_RESID) ? 2 : 0) + ((EPI & CG_EPI_DGELU) ? W : 0) +
+                                      ((EPI & CG_EPI_ACCUM) ? 2 : 0)) + ((EPI & CG_EPI_BIAS) ? 4 : 0);
+  // epilogue STORES (C, GELU pre-activation, column-sum partials; SwiGLU: g, u, s per row chunk /
+  // d(g), d(u) per chunk), issued after the last k-step
+  static constexpr int S = SWG ? 12 : DSW ? 16 : 8 * (W + ((EPI & CG_EPI_GELU) ? W : 0)) + ((EPI & CG_EPI_COLSUM) ? 4 : 0);
 };
+// SwiGLU B image: tile row r holds B row ((r >> 5) & 1) * N + 32 (r >> 6) + (r & 31) of [gate; up]
+// (N rows each), so a wave's column chunk c = 0 is gate j and c = 1 is up j for the same j
+__device__ __forceinline__ uint32_t b_src_off_swg(int pos, long long ld, int N) {
+  const int row = pos >> 7, phys = (pos >> 4) & 7;
+  const int brow = ((row >> 5) & 1) * N + 32 * (row >> 6) + (row & 31);
+  return (uint32_t)(((long long)brow * ld + 8 * (phys ^ fb(row))) * 2);
+}
 
 __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -104,11 +114,13 @@ template <int EPI, int CT>
 __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
   using namespace bfp;
   constexpr int NL = Epi<EPI, CT>::L, NS = Epi<EPI, CT>::S;
+  constexpr bool SWG = Epi<EPI, CT>::SWG, DSW = Epi<EPI, CT>::DSW;
+  constexpr int BNO = SWG ? BN / 2 : BN;  // output columns per tile (SwiGLU: 64 s-columns from 128 B rows)
   constexpr int ES = CT == CG_BF16 ? 2 : 4;
   static_assert(NL + NS + DMA_PER_STAGE <= 63, "vmcnt range");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int tiles_n = (p.N + BN - 1) / BN, tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.N + BNO - 1) / BNO, tiles_m = (p.M + BM - 1) / BM;
   const int ntiles = tiles_n * tiles_m;
   const int nblk = gridDim.x;
   const int lb = cg_xcd_remap(blockIdx.x, nblk);  // an XCD's blocks walk contiguous tile ranges
@@ -118,17 +130,20 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
 
   const __amdgpu_buffer_rsrc_t ra = rsrc(p.A, ((long long)(p.M - 1) * p.lda + p.K) * 2);
-  const __amdgpu_buffer_rsrc_t rb = rsrc(p.B, ((long long)(p.N - 1) * p.ldb + p.K) * 2);
+  const __amdgpu_buffer_rsrc_t rb = rsrc(p.B, ((long long)((SWG ? 2 : 1) * p.N - 1) * p.ldb + p.K) * 2);
   uint32_t va[A_CHUNKS], vb[B_CHUNKS];
 #pragma unroll
   for (int i = 0; i < A_CHUNKS; ++i) va[i] = bfw::src_off<true>((wave + WAVES * i) * 1024 + 16 * lane, p.lda);
 #pragma unroll
-  for (int i = 0; i < B_CHUNKS; ++i) vb[i] = b_src_off((wave + WAVES * i) * 1024 + 16 * lane, p.ldb);
+  for (int i = 0; i < B_CHUNKS; ++i) {
+    const int pos = (wave + WAVES * i) * 1024 + 16 * lane;
+    vb[i] = SWG ? b_src_off_swg(pos, p.ldb, p.N) : b_src_off(pos, p.ldb);
+  }
 
   auto tile_org = [&](int k, int& m0, int& n0) {
     const int tile = lb + k * nblk;
     m0 = (tile / tiles_n) * BM;
-    n0 = (tile % tiles_n) * BN;
+    n0 = (tile % tiles_n) * BNO;
   };
   // DMA source origins of global k-step g (OOR past the end: the DMA then fills a free slot with zeros)
   auto stage_org = [&](int g, uint32_t& ao, uint32_t& bo) {
@@ -154,7 +169,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 
   // epilogue of local tile k straight from the accumulators: lane owns rows
   // m0+wm+16i+(l&15) (i = 0..3) x columns n0+wn+32c+8(l>>4)+[0,8) (c = 0..1)
-  const __amdgpu_buffer_rsrc_t rc = rsrc(p.C, ((long long)(p.M - 1) * p.ldc + p.N) * ES);
+  const __amdgpu_buffer_rsrc_t rc = rsrc(p.C, ((long long)(p.M - 1) * p.ldc + (DSW ? 2 : 1) * p.N) * ES);
   const int g4 = lane >> 4, r16 = lane & 15;
   u32x4 xa[4][2], xb[4][2], bq[2][2];
   uint32_t off_c[4][2];
@@ -167,7 +182,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     bool cok[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      col[c] = n0 + wn + 32 * c + 8 * g4;
+      col[c] = SWG ? n0 + (wn >> 1) + 8 * g4 : n0 + wn + 32 * c + 8 * g4;
       cok[c] = col[c] < p.N;
     }
     if constexpr ((EPI & CG_EPI_BIAS) != 0) {
@@ -202,6 +217,12 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
         if constexpr ((EPI & CG_EPI_ACCUM) != 0) {
           xa[i][c] = bld(rc, off_c[i][c]);
           xb[i][c] = bld(rc, off_c[i][c] + 16);
+        }
+        if constexpr (DSW) {  // gate at column col, up at N + col of aux
+          const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux, ((long long)(p.M - 1) * p.ld_aux + 2 * p.N) * 2);
+          const uint32_t o = ok ? (uint32_t)(((long long)row * p.ld_aux + col[c]) * 2) : OOR;
+          xa[i][c] = bld(rx, o);
+          xb[i][c] = bld(rx, ok ? o + (uint32_t)p.N * 2u : OOR);
         }
       }
     }
@@ -270,6 +291,58 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int j = 0; j < 8; ++j) csum[c][j] = 0.f;
+    }
+    if constexpr (SWG) {
+      // chunk 0 = gate, chunk 1 = up of the same 8 columns j: pre-activations to aux_out (g at j,
+      // u at N + j), s = silu(g) * u to C (0 past n_valid)
+      const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux_out, ((long long)(p.M - 1) * p.ld_aux + 2 * p.N) * 2);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm + 16 * i + r16;
+        float g[8], u[8], sv[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            g[4 * h + q] = acc[i][h][q];
+            u[4 * h + q] = acc[i][2 + h][q];
+          }
+        const bool ok = off_c[i][0] != OOR;
+        const uint32_t o = ok ? (uint32_t)(((long long)row * p.ld_aux + col[0]) * 2) : OOR;
+        bst(rx, o, pack_bf16(g));
+        bst(rx, ok ? o + (uint32_t)p.N * 2u : OOR, pack_bf16(u));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sv[j] = col[0] + j < p.n_valid ? silu_f(g[j]) * u[j] : 0.f;
+        bst(rc, off_c[i][0], pack_bf16(sv));
+      }
+      return;
+    } else if constexpr (DSW) {
+      // v = dL/ds for columns j: d(g) to C at j, d(u) to C at N + j (0 past n_valid)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          float v[8], g[8], u[8], dg[8], du[8];
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[4 * h + q] = acc[i][2 * c + h][q];
+          unpack_bf16(xa[i][c], g);
+          unpack_bf16(xb[i][c], u);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            dg[j] = du[j] = 0.f;
+            if (col[c] + j < p.n_valid) {
+              const float sg = 1.0f / (1.0f + __expf(-g[j]));
+              du[j] = v[j] * (g[j] * sg);
+              dg[j] = v[j] * u[j] * sg * (1.0f + g[j] * (1.0f - sg));
+            }
+          }
+          bst(rc, off_c[i][c], pack_bf16(dg));
+          bst(rc, off_c[i][c] == OOR ? OOR : off_c[i][c] + (uint32_t)p.N * 2u, pack_bf16(du));
+        }
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {

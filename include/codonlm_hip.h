@@ -33,9 +33,14 @@ enum {
   CG_EPI_RESID = 8,      /* out = resid[m,n] + v   (resid fp32, may alias C)           */
   CG_EPI_DROPOUT = 16,   /* v = v * keep(seed, m, n) / (1-p) before RESID              */
   CG_EPI_ACCUM = 32,     /* out (fp32) += v                                            */
-  CG_EPI_COLSUM = 64     /* also column sums of the final values into `workspace` as    */
+  CG_EPI_COLSUM = 64,    /* also column sums of the final values into `workspace` as    */
                          /* [ceil(M/64)][N] fp32 partials (reduce: cg_colsum_reduce) --  */
                          /* a fused bias gradient; needs split_k == 1                     */
+  /* SwiGLU (model_tiny_gpt.py:47-57), bf16 persistent tile only (else CG_EUNSUPPORTED): */
+  CG_EPI_SWIGLU = 128,   /* B = [w_gate; w_up] (2N rows): aux_out [M][2N] receives the  */
+                         /* pre-activations g|u, C [M][N] = silu(g) * u (0 for n >= n_valid) */
+  CG_EPI_DSWIGLU = 256   /* v = dL/ds; aux = g|u [M][2N]: C [M][2N] = d(g|u)             */
+                         /* (0 for n >= n_valid)                                         */
 };
 
 /*
@@ -60,6 +65,7 @@ typedef struct {
   const void* aux; void* aux_out; long long ld_aux;
   uint32_t drop_seed; float drop_p;
   int split_k; float* workspace;
+  int n_valid; /* SWIGLU / DSWIGLU: columns < n_valid are live (0 = all N) */
 } cg_gemm_desc;
 int cg_gemm(const cg_gemm_desc* d, void* stream);
 /* bf16 tile selection: -1 auto (default; env CG_GEMM_WIDE overrides at load), 0 = 128x128

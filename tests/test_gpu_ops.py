@@ -186,6 +186,47 @@ def test_swiglu_fwd_bwd(dtype, H, Hp, ld_pad):
     assert torch.all(d[:, H:Hp] == 0) and torch.all(d[:, Hp + H:] == 0)
 
 
+@pytest.mark.parametrize("M,Hp,H,K", [(1024, 1024, 1024, 384), (700, 1408, 1365, 512), (256, 128, 100, 128)])
+def test_gemm_swiglu_epilogues(M, Hp, H, K):
+    """The gate|up product with SwiGLU in the persistent tile's epilogue (CG_EPI_SWIGLU: B rows
+    remapped so one lane holds gate j and up j) and the dL/ds product with the SwiGLU backward in
+    its epilogue (CG_EPI_DSWIGLU), against the separate passes (cg_swiglu_fwd / _bwd) on the same
+    bf16 products."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    g = torch.Generator().manual_seed(M + Hp)
+    x = (torch.randn(M, K, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    wgu = torch.randn(2 * Hp, K, generator=g) * K ** -0.5
+    wgu[H:Hp] = 0
+    wgu[Hp + H:] = 0
+    wgu = wgu.to(DEV, torch.bfloat16)
+    gu_ref = ops.gemm(x, wgu)                                  # [M][2Hp]
+    s_ref = ops.swiglu_fwd(gu_ref, H)
+    gu = torch.full((M, 2 * Hp), float("nan"), device=DEV, dtype=torch.bfloat16)
+    s = ops.gemm(x, wgu, N=Hp, epilogue=L.EPI_SWIGLU, aux_out=gu, n_valid=H)
+    torch.cuda.synchronize()
+    assert torch.equal(gu, gu_ref)  # same products, same k order: bitwise
+    # s from the unrounded fp32 g, u (the separate pass reads them in bf16): bf16-rounding close
+    err = (s.float() - s_ref.float()).abs().max().item()
+    assert err <= 1.6e-2 * (1 + s_ref.float().abs().max().item()), err
+    assert torch.all(s[:, H:] == 0)
+    # backward: dL/ds = gin . wd  (wd [d][Hp], K-contiguous operand wd^T [Hp][d])
+    dmod = K
+    gin = torch.randn(M, dmod, generator=g).to(DEV, torch.bfloat16)
+    wdT = (torch.randn(Hp, dmod, generator=g) * dmod ** -0.5).to(DEV, torch.bfloat16)
+    ds = ops.gemm(gin, wdT)                                    # [M][Hp]
+    dgu_ref = ops.swiglu_bwd(gu_ref, ds, H)
+    dgu = torch.full((M, 2 * Hp), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.gemm(gin, wdT, N=Hp, out=dgu, epilogue=L.EPI_DSWIGLU, aux=gu_ref, n_valid=H)
+    torch.cuda.synchronize()
+    # same fp32 product, dgu computed from it before rounding (the separate pass reads ds in
+    # bf16): equal to bf16 rounding
+    ref = dgu_ref.float()
+    err = (dgu.float() - ref).abs().max().item()
+    assert err <= 1.6e-2 * (1 + ref.abs().max().item()), err
+    assert torch.all(dgu[:, H:Hp] == 0) and torch.all(dgu[:, Hp + H:] == 0)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("H,KV,hd", [(8, 4, 48), (4, 4, 64), (2, 1, 20)])
 def test_rope_forward_inverse(dtype, H, KV, hd):
