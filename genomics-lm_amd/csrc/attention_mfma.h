@@ -24,6 +24,17 @@
 #define ATTN_DQ_WPS 3  // waves per SIMD the dQ kernel is register-limited to (<= 168 VGPRs)
 #endif
 
+// ATTN_PRIO: raise a wave's issue priority while it issues its MFMA chains (s_setprio), so the
+// SIMD's other wave fills the gaps with VALU work instead of delaying them (A/B variant)
+#ifndef ATTN_PRIO
+#define ATTN_PRIO 0
+#endif
+#if ATTN_PRIO
+#define ATTN_SETPRIO(x) __builtin_amdgcn_s_setprio(x)
+#else
+#define ATTN_SETPRIO(x) ((void)0)
+#endif
+
 namespace fa {
 constexpr int HDP = 64;        // padded head dim held in LDS / registers
 constexpr int KT = 64;         // rows per staged tile
@@ -462,15 +473,18 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       pa = keep_b(pa, 0, w);
       pb = keep_b(pb, 1, w);
     }
+    ATTN_SETPRIO(1);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 0), pa, o0, 0, 0, 0);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 0), pb, o0, 0, 0, 0);
     if constexpr (hd > 32) {
       o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 1), pa, o1, 0, 0, 0);
       o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 1), pb, o1, 0, 0, 0);
     }
+    ATTN_SETPRIO(0);
   };
   auto body = [&](const char* Ki, const char* Vi, int k0, uint2 wc, auto full_c) __attribute__((always_inline)) {
     v16f s0 = zero16(), s1 = zero16();
+    ATTN_SETPRIO(1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
       if (ks < nks) s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, 0, ks), qf[ks], s0, 0, 0, 0);
@@ -479,6 +493,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
     for (int ks = 0; ks < 4; ++ks)
       if (ks < nks) s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, 32, ks), qf[ks], s1, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
+    ATTN_SETPRIO(0);
     // S feeds inline asm (max3): hipcc pads the XDL-result -> VALU-read hazard only before its own
     // instructions, so each half's accumulator passes through a wait of 19 states first (>= the
     // 16-pass rule); without it v_max3 can read a stale accumulator and the row max varies run to run
@@ -649,6 +664,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
     auto body = [&](bool full) __attribute__((always_inline)) {
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
+        ATTN_SETPRIO(1);
         v16f s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, lsefrag, zero16(), 0, 0, 0);
         v16f dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, ndfrag, zero16(), 0, 0, 0);
 #pragma unroll
@@ -658,6 +674,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Vi, ro, kb * 32, ks), df[ks], dp, 0, 0, 0);
           }
         }
+        ATTN_SETPRIO(0);
         const int kq = myq - k0 - kb * 32, kl = lo - k0 - kb * 32;
         if (!full) {
 #pragma unroll
@@ -687,12 +704,14 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
           }
         }
         const v8bf b0 = pack_b(s, 0), b1 = pack_b(s, 1);
+        ATTN_SETPRIO(1);
         a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 0), b0, a0, 0, 0, 0);
         a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 0), b1, a0, 0, 0, 0);
         if constexpr (hd > 32) {
           a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 1), b0, a1, 0, 0, 0);
           a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 1), b1, a1, 0, 0, 0);
         }
+        ATTN_SETPRIO(0);
       }
     };
     if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) body((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max));
@@ -881,6 +900,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
           s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
         }
         v16f dp = nd;
+        ATTN_SETPRIO(1);
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
           if (ks < nks) {
@@ -888,6 +908,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
           }
         }
+        ATTN_SETPRIO(0);
         if (!full) {
 #pragma unroll
           for (int rg = 0; rg < 16; rg += 4) {
@@ -934,6 +955,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         }
         const v8bf pb0 = pack_b(pd, 0), pb1 = pack_b(pd, 1);
         const v8bf sb0 = pack_b(s, 0), sb1 = pack_b(s, 1);
+        ATTN_SETPRIO(1);
         dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 0), pb0, dv0, 0, 0, 0);
         dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 0), pb1, dv0, 0, 0, 0);
         dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 0), sb0, dk0, 0, 0, 0);
@@ -944,6 +966,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
           dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 1), sb0, dk1, 0, 0, 0);
           dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 1), sb1, dk1, 0, 0, 0);
         }
+        ATTN_SETPRIO(0);
       }
     };
     if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (los[qlast - q0] <= kw0));
