@@ -21,7 +21,9 @@
 #define ATTN_FWD_WPS 2
 #endif
 #ifndef ATTN_DQ_WPS
-#define ATTN_DQ_WPS 3  // waves per SIMD the dQ kernel is register-limited to (<= 168 VGPRs)
+// waves per SIMD the dQ kernel is register-limited to: 3 (<= 168 VGPRs) spilled once S and dP were
+// seeded by MFMAs; 2 measured 3-5 % faster on the C4 backward (tools/attn_time.py, same box)
+#define ATTN_DQ_WPS 2
 #endif
 
 // ATTN_PRIO: raise a wave's issue priority while it issues its MFMA chains (s_setprio), so the
