@@ -233,6 +233,8 @@ struct Acts {
   bool wT;  // transposed weight copies present
   // auxiliary offset heads: pre-GELU a, GELU output g, projection pj (compute dtype, M x d)
   std::vector<void*> oa, og, opj;
+  // their backward dY operands, kept per head until one grouped dW launch takes all of them
+  std::vector<void*> odpj, oda;
 };
 
 constexpr int MAX_SPLIT = 16;
@@ -272,7 +274,10 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.logits_pad = w.take<float>(M * D.Vp * 4);  // head product at N = Vp (vector-epilogue tiles)
   const int noff = std::min(c->n_offsets, 8);
   A.oa.assign(noff, nullptr); A.og.assign(noff, nullptr); A.opj.assign(noff, nullptr);
+  A.odpj.assign(noff, nullptr); A.oda.assign(noff, nullptr);
   for (int i = 0; i < noff; ++i) {
+    A.odpj[i] = w.take<char>(M * d * es);
+    A.oda[i] = w.take<char>(M * d * es);
     A.oa[i] = w.take<char>(M * d * es);
     A.og[i] = w.take<char>(M * d * es);
     A.opj[i] = w.take<char>(M * d * es);
@@ -628,6 +633,22 @@ int aux_backward(const Ctx& C, int accumulate) {
     }
   }
   const int noff = std::min(m->cfg.n_offsets, 8);
+  // the offset heads' two d x d weight gradients each (bf16: one grouped launch after the loop,
+  // as the blocks' dW; their dY operands stay in per-head buffers)
+  cg_dw_group grp;
+  memset(&grp, 0, sizeof(grp));
+  grp.K = (int)M;
+  grp.tile_m = 128;  // 10 products of d x d at C5: the 128-row tile gives the most workgroups
+  auto add_dw = [&](const void* dy, const void* x, long long goff) -> int {
+    if (C.dt != CG_BF16) return lin_dw(C, dy, d, x, d, d, d, goff, d, accumulate);
+    cg_dw_product& q = grp.p[grp.n++];
+    q.A = dy; q.lda = d;
+    q.B = x; q.ldb = d;
+    q.C = G(C, goff); q.ldc = d;
+    q.N_out = d; q.K_out = d;
+    q.alpha = 1.0f; q.accumulate = accumulate;
+    return CG_OK;
+  };
   for (int i = 0; i < noff; ++i) {
     const float* dl = m->d_offset_logits[i];
     if (!dl) {
@@ -653,22 +674,34 @@ int aux_backward(const Ctx& C, int accumulate) {
     g.workspace = A.splitws;
     CK(cg_gemm(&g, C.s));
     // dpj = Gc . E ; the second Linear's grads
-    g = head_dx(C, hoff, A.dsmall, d);
+    void* dpj = A.odpj[i];
+    void* da = A.oda[i];
+    g = head_dx(C, hoff, dpj, d);
     g.c_dtype = C.dt;
     CK(cg_gemm(&g, C.s));
-    CK(lin_dw(C, A.dsmall, d, A.og[i], d, d, d, C.Lo.off2w[i], d, accumulate));
-    CK(bias_grad(C, A.dsmall, d, d, C.Lo.off2b[i], accumulate));
+    CK(add_dw(dpj, A.og[i], C.Lo.off2w[i]));
+    CK(bias_grad(C, dpj, d, d, C.Lo.off2b[i], accumulate));
     // da = (dpj . W2) * gelu'(a) ; the first Linear's grads
-    g = lin_dx(C, A.dsmall, d, C.Lo.off2w[i], d, d, d, A.dbig, d);
+    g = lin_dx(C, dpj, d, C.Lo.off2w[i], d, d, d, da, d);
     g.epilogue = CG_EPI_DGELU; g.aux = A.oa[i]; g.ld_aux = d;
     CK(cg_gemm(&g, C.s));
-    CK(lin_dw(C, A.dbig, d, A.xf, d, d, d, C.Lo.off1w[i], d, accumulate));
-    CK(bias_grad(C, A.dbig, d, d, C.Lo.off1b[i], accumulate));
+    CK(add_dw(da, A.xf, C.Lo.off1w[i]));
+    CK(bias_grad(C, da, d, d, C.Lo.off1b[i], accumulate));
     // dxf += da . W1
-    g = lin_dx(C, A.dbig, d, C.Lo.off1w[i], d, d, d, A.dtmp, d);
+    g = lin_dx(C, da, d, C.Lo.off1w[i], d, d, d, A.dtmp, d);
     g.c_dtype = CG_F32;
     g.epilogue = CG_EPI_RESID; g.resid = A.dtmp; g.ldr = d;
     CK(cg_gemm(&g, C.s));
+  }
+  if (grp.n) {
+    int rc = cg_gemm_dw_grouped(&grp, C.s);
+    for (int j = 0; rc == CG_EUNSUPPORTED && j < grp.n; ++j) {  // unaligned shapes: per product
+      const cg_dw_product& q = grp.p[j];
+      const int r2 = lin_dw(C, q.A, q.lda, q.B, q.ldb, q.N_out, q.K_out, q.C - m->grads, q.ldc, accumulate);
+      if (r2 != CG_OK) return r2;
+      if (j == grp.n - 1) rc = CG_OK;
+    }
+    CK(rc);
   }
   return CG_OK;
 }
