@@ -235,6 +235,9 @@ struct Acts {
   std::vector<void*> oa, og, opj;
   // their backward dY operands, kept per head until one grouped dW launch takes all of them
   std::vector<void*> odpj, oda;
+  // per offset head: its logits gradient (the layout of dlogits), stacked [head][M] like opj, so
+  // the tied head's weight gradient over all heads is ONE product reduced over heads x tokens
+  std::vector<void*> odl;
 };
 
 constexpr int MAX_SPLIT = 16;
@@ -274,13 +277,18 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.logits_pad = w.take<float>(M * D.Vp * 4);  // head product at N = Vp (vector-epilogue tiles)
   const int noff = std::min(c->n_offsets, 8);
   A.oa.assign(noff, nullptr); A.og.assign(noff, nullptr); A.opj.assign(noff, nullptr);
-  A.odpj.assign(noff, nullptr); A.oda.assign(noff, nullptr);
+  A.odpj.assign(noff, nullptr); A.oda.assign(noff, nullptr); A.odl.assign(noff, nullptr);
+  const size_t es_dl = c->dtype == CG_BF16 ? 2 : 4;
+  const long long ldl_ = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
+  char* opj_all = noff ? w.take<char>((size_t)noff * M * d * es) : nullptr;
+  char* odl_all = noff ? w.take<char>((size_t)noff * M * ldl_ * es_dl) : nullptr;
   for (int i = 0; i < noff; ++i) {
+    A.opj[i] = opj_all + (size_t)i * M * d * es;
+    A.odl[i] = odl_all + (size_t)i * M * ldl_ * es_dl;
     A.odpj[i] = w.take<char>(M * d * es);
     A.oda[i] = w.take<char>(M * d * es);
     A.oa[i] = w.take<char>(M * d * es);
     A.og[i] = w.take<char>(M * d * es);
-    A.opj[i] = w.take<char>(M * d * es);
   }
   A.ldl = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
   A.dlogits = w.take<char>(M * A.ldl * es);
@@ -416,12 +424,13 @@ cg_gemm_desc lin_dx(const Ctx& C, const void* dy, long long lddy, long long woff
 // d[M,d] (fp32, + resid epilogue set by the caller) = dl[M,Vp] . E[Vp,d] for a head weight E:
 // in bf16 mode dl holds split-bf16 rows (hi | lo, CG_BF16X2) and the product runs over
 // K = 2 Vp against [E; E] (A.head2, filled by fill_head2)
-cg_gemm_desc head_dx(const Ctx& C, long long hoff, void* out, long long ldo) {
+cg_gemm_desc head_dx(const Ctx& C, long long hoff, void* out, long long ldo, const void* dl = nullptr) {
   const Dims& D = C.D;
-  if (C.dt != CG_BF16) return lin_dx(C, C.A.dlogits, D.Vp, hoff, D.d, D.Vp, D.d, out, ldo);
+  if (!dl) dl = C.A.dlogits;
+  if (C.dt != CG_BF16) return lin_dx(C, dl, D.Vp, hoff, D.d, D.Vp, D.d, out, ldo);
   cg_gemm_desc g = gdesc(C);
   g.M = (int)C.M; g.N = D.d; g.K = 2 * D.Vp;
-  g.A = C.A.dlogits; g.lda = C.A.ldl; g.a_kcontig = 1;
+  g.A = dl; g.lda = C.A.ldl; g.a_kcontig = 1;
   g.B = C.A.head2; g.ldb = D.d; g.b_kcontig = 0;
   g.C = out; g.ldc = ldo;
   return g;
@@ -661,22 +670,11 @@ int aux_backward(const Ctx& C, int accumulate) {
       continue;
     }
     if (!m->aux_ready) return CG_EINVAL;
-    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, D.Vp, C.s));
-    // d(head) += Gc^T . pj   (phase 0's own head product initialised it; hi half of split rows)
-    cg_gemm_desc g = gdesc(C);
-    g.c_dtype = CG_F32;
-    g.M = D.Vp; g.N = d; g.K = (int)M;
-    g.A = A.dlogits; g.lda = A.ldl; g.a_kcontig = 0;
-    g.B = A.opj[i]; g.ldb = d; g.b_kcontig = 0;
-    g.C = G(C, hoff); g.ldc = d;
-    g.epilogue = CG_EPI_ACCUM;
-    g.split_k = pick_split(C, D.Vp, d, M);
-    g.workspace = A.splitws;
-    CK(cg_gemm(&g, C.s));
+    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.odl[i], A.ldl, D.Vp, C.s));
     // dpj = Gc . E ; the second Linear's grads
     void* dpj = A.odpj[i];
     void* da = A.oda[i];
-    g = head_dx(C, hoff, dpj, d);
+    cg_gemm_desc g = head_dx(C, hoff, dpj, d, A.odl[i]);
     g.c_dtype = C.dt;
     CK(cg_gemm(&g, C.s));
     CK(add_dw(dpj, A.og[i], C.Lo.off2w[i]));
@@ -692,6 +690,32 @@ int aux_backward(const Ctx& C, int accumulate) {
     g.c_dtype = CG_F32;
     g.epilogue = CG_EPI_RESID; g.resid = A.dtmp; g.ldr = d;
     CK(cg_gemm(&g, C.s));
+  }
+  // d(head) += sum_i Gc_i^T . pj_i over the heads with a gradient: one product reduced over
+  // (head, token) rows -- the logits gradients and pj operands are stacked per head (phase 0's own
+  // head product initialised it; hi half of split rows)
+  for (int first = 0; first < noff;) {  // one product per run of consecutive heads with a gradient
+    if (!m->d_offset_logits[first]) {
+      ++first;
+      continue;
+    }
+    int cnt = 1;
+    while (first + cnt < noff && m->d_offset_logits[first + cnt]) ++cnt;
+    cg_gemm_desc g = gdesc(C);
+    g.c_dtype = CG_F32;
+    g.M = D.Vp; g.N = d; g.K = (int)(M * cnt);
+    g.A = A.odl[first]; g.lda = A.ldl; g.a_kcontig = 0;
+    g.B = A.opj[first]; g.ldb = d; g.b_kcontig = 0;
+    g.C = G(C, hoff); g.ldc = d;
+    g.epilogue = CG_EPI_ACCUM;
+    // a few output tiles over a long reduction: more slabs than pick_split's cap (16) so the
+    // launch fills the chip (~1 k-row per slab), bounded by the slab workspace
+    long long sk = std::max<long long>(pick_split(C, D.Vp, d, M * cnt), std::min<long long>(96, M * cnt / 1024));
+    while (sk > 1 && (size_t)sk * D.Vp * d > A.splitws_floats) --sk;
+    g.split_k = (int)sk;
+    g.workspace = A.splitws;
+    CK(cg_gemm(&g, C.s));
+    first += cnt;
   }
   if (grp.n) {
     int rc = cg_gemm_dw_grouped(&grp, C.s);
