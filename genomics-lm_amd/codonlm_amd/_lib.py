@@ -145,6 +145,7 @@ SIGNATURES = {
     "cg_colsum_workspace": (sz, [i32, i32]),
     "cg_colsum": (i32, [i32, vp, i64, i32, i32, vp, i32, vp, vp]),
     "cg_colsum_reduce": (i32, [vp, i32, i32, vp, i32, vp]),
+    "cg_colsum_partials": (i32, [i32, vp, i64, i32, i32, vp, C.POINTER(i32), vp]),
     "cg_cast_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),

@@ -238,6 +238,7 @@ struct Acts {
   // per offset head: its logits gradient (the layout of dlogits), stacked [head][M] like opj, so
   // the tied head's weight gradient over all heads is ONE product reduced over heads x tokens
   std::vector<void*> odl;
+  std::vector<float*> ocp;  // their bias-gradient column-sum partials (2 per head), reduced batched
 };
 
 constexpr int MAX_SPLIT = 16;
@@ -278,11 +279,13 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   const int noff = std::min(c->n_offsets, 8);
   A.oa.assign(noff, nullptr); A.og.assign(noff, nullptr); A.opj.assign(noff, nullptr);
   A.odpj.assign(noff, nullptr); A.oda.assign(noff, nullptr); A.odl.assign(noff, nullptr);
+  A.ocp.assign(noff, nullptr);
   const size_t es_dl = c->dtype == CG_BF16 ? 2 : 4;
   const long long ldl_ = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
   char* opj_all = noff ? w.take<char>((size_t)noff * M * d * es) : nullptr;
   char* odl_all = noff ? w.take<char>((size_t)noff * M * ldl_ * es_dl) : nullptr;
   for (int i = 0; i < noff; ++i) {
+    A.ocp[i] = w.take<float>(2 * cg_colsum_workspace((int)M, d));
     A.opj[i] = opj_all + (size_t)i * M * d * es;
     A.odl[i] = odl_all + (size_t)i * M * ldl_ * es_dl;
     A.odpj[i] = w.take<char>(M * d * es);
@@ -312,7 +315,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.delta = w.take<float>((size_t)B * D.H * T * 4);
   A.lnpart = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
   const long long maxcols = std::max<long long>({big, (long long)d, (long long)D.Hp});
-  A.colws = w.take<float>((size_t)64 * maxcols * 4);
+  A.colws = w.take<float>(cg_colsum_workspace((int)M, (int)maxcols));
   A.bpart = w.take<float>((size_t)B * ((T + 127) / 128) * D.Nqkv * 4);
   long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,
                                         (long long)D.Vp * d, (long long)d * d});
@@ -562,6 +565,13 @@ int ln_bwd_deferred(const Ctx& C, int dy_dtype, const void* dy, const float* x, 
   return CG_OK;
 }
 
+// column sums of dy [M][d] (a bias gradient) as partial rows joining the pending batch
+int defer_colsum(const Ctx& C, const void* dy, float* part, long long goff, int accumulate) {
+  int np = 0;
+  CK(cg_colsum_partials(C.dt, dy, C.D.d, (int)C.M, C.D.d, part, &np, C.s));
+  return defer_reduce(C.m, part, C.D.d, np, C.D.d, G(C, goff), accumulate, C.s);
+}
+
 // The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
 // bf16 mode (gemm_dw.h), the per-product GEMMs in fp32 parity mode.
 int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
@@ -678,13 +688,13 @@ int aux_backward(const Ctx& C, int accumulate) {
     g.c_dtype = C.dt;
     CK(cg_gemm(&g, C.s));
     CK(add_dw(dpj, A.og[i], C.Lo.off2w[i]));
-    CK(bias_grad(C, dpj, d, d, C.Lo.off2b[i], accumulate));
+    CK(defer_colsum(C, dpj, A.ocp[i], C.Lo.off2b[i], accumulate));
     // da = (dpj . W2) * gelu'(a) ; the first Linear's grads
     g = lin_dx(C, dpj, d, C.Lo.off2w[i], d, d, d, da, d);
     g.epilogue = CG_EPI_DGELU; g.aux = A.oa[i]; g.ld_aux = d;
     CK(cg_gemm(&g, C.s));
     CK(add_dw(da, A.xf, C.Lo.off1w[i]));
-    CK(bias_grad(C, da, d, d, C.Lo.off1b[i], accumulate));
+    CK(defer_colsum(C, da, A.ocp[i] + cg_colsum_workspace((int)M, d) / 4, C.Lo.off1b[i], accumulate));
     // dxf += da . W1
     g = lin_dx(C, da, d, C.Lo.off1w[i], d, d, d, A.dtmp, d);
     g.c_dtype = CG_F32;
@@ -992,6 +1002,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xL, d, A.meanf, A.rstdf, P(C, C.Lo.lnfw), nullptr, A.g, C.dt,
                         D.L > 0 ? A.slot[slot_of(D, ll)].gin : nullptr, site_seed(seed, ll, SITE_MLP), D.L > 0 ? p : 0.f, A.lnpart,
                         G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), db2, accumulate, (int)M, d, eps, C.s));
+    CK(flush_reduce(m, C.s));  // the aux heads' bias gradients (their bucket is complete here)
     return CG_OK;
   }
   if (phase == 1) {

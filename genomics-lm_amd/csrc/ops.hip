@@ -1056,7 +1056,8 @@ extern "C" int cg_swiglu_bwd(int dtype, const void* gu, long long ldgu, int Hp, 
 constexpr int COLSUM_R = 64;
 extern "C" size_t cg_colsum_workspace(int rows, int cols) {
   (void)rows;
-  return (size_t)COLSUM_R * cols * sizeof(float);
+  const int nrb = rows > 0 ? (rows + 127) / 128 : 1;  // colsum_vec_kernel's 128-row blocks
+  return (size_t)(nrb > COLSUM_R ? nrb : COLSUM_R) * cols * sizeof(float);
 }
 template <typename T_>
 __global__ __launch_bounds__(256) void colsum_part_kernel(const T_* __restrict__ X, long long ldx, int rows, int cols,
@@ -1105,13 +1106,15 @@ extern "C" int cg_colsum_reduce(const float* part, int nparts, int cols, float* 
 // Fast path: 8 columns (one 16-B bf16 chunk / two float4) per thread, 32 column chunks x
 // 8 row lanes per 256-thread block, COLSUM_RB rows per block; partial rows reduced by
 // colsum_reduce_kernel.
-constexpr int COLSUM_RB = 512;
+// 128-row x 128-column blocks: 16 column chunks of 8 x 16 row lanes (C5's d = 384 bias sums ran
+// as 64 workgroups of 512 rows x 256 columns, half of them half empty)
+constexpr int COLSUM_RB = 128;
 template <typename T_>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(const T_* __restrict__ X, long long ldx, int rows, int cols,
                                                          float* __restrict__ part) {
-  __shared__ float red[8][256 + 8];
-  const int ch = threadIdx.x & 31, rs = threadIdx.x >> 5;
-  const int c0 = blockIdx.x * 256 + ch * 8;
+  __shared__ float red[16][128 + 4];
+  const int ch = threadIdx.x & 15, rs = threadIdx.x >> 4;
+  const int c0 = blockIdx.x * 128 + ch * 8;
   const int r0 = blockIdx.y * COLSUM_RB;
   const int r1 = min(rows, r0 + COLSUM_RB);
   float acc[8];
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(const T_* __restrict__ 
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
   if (c0 < cols) {
 #pragma unroll 4
-    for (int r = r0 + rs; r < r1; r += 8) {
+    for (int r = r0 + rs; r < r1; r += 16) {
       const T_* p = X + (long long)r * ldx + c0;
       if (sizeof(T_) == 2) {
         const uint4 u = *(const uint4*)p;
@@ -1139,42 +1142,60 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(const T_* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 8; ++j) red[rs][ch * 8 + j] = acc[j];
   __syncthreads();
-  const int c = threadIdx.x;  // one output column per thread
-  if (blockIdx.x * 256 + c < cols) {
-    float v = 0.f;
+  if (threadIdx.x < 128) {  // one output column per thread, fixed order
+    const int c = threadIdx.x;
+    if (blockIdx.x * 128 + c < cols) {
+      float v = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) v += red[i][c];
-    part[(long long)blockIdx.y * cols + blockIdx.x * 256 + c] = v;
+      for (int i = 0; i < 16; ++i) v += red[i][c];
+      part[(long long)blockIdx.y * cols + blockIdx.x * 128 + c] = v;
+    }
   }
+}
+
+static inline bool colsum_vec_ok(const void* X, long long ldx, int cols) {
+  return cols % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0;
+}
+
+extern "C" int cg_colsum_partials(int dtype, const void* X, long long ldx, int rows, int cols, float* part,
+                                  int* nparts, void* stream) {
+  if (!nparts || (cols > 0 && (!X || !part))) return CG_EINVAL;
+  *nparts = 0;
+  if (cols <= 0 || rows <= 0) return CG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (colsum_vec_ok(X, ldx, cols)) {
+    const int nrb = cg_cdiv(rows, COLSUM_RB);
+    dim3 g(cg_cdiv(cols, 128), nrb);
+    if (dtype == CG_BF16)
+      hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)X, ldx, rows, cols, part);
+    else
+      hipLaunchKernelGGL(colsum_vec_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, part);
+    *nparts = nrb;
+  } else {
+    const int nch = rows < COLSUM_R ? rows : COLSUM_R;
+    dim3 g(cg_cdiv(cols, 256), nch);
+    if (dtype == CG_BF16)
+      hipLaunchKernelGGL(colsum_part_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)X, ldx, rows, cols, part);
+    else
+      hipLaunchKernelGGL(colsum_part_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, part);
+    *nparts = nch;
+  }
+  CG_LAUNCH_CHECK();
+  return CG_OK;
 }
 
 extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out, int accumulate,
                          void* ws, void* stream) {
   if (cols == 0) return CG_OK;
-  hipStream_t s = (hipStream_t)stream;
-  const int nrb = cg_cdiv(rows > 0 ? rows : 1, COLSUM_RB);
-  if (cols % 8 == 0 && ldx % 8 == 0 && ((uintptr_t)X & 15) == 0 && nrb <= COLSUM_R) {
-    dim3 g(cg_cdiv(cols, 256), nrb);
-    if (dtype == CG_BF16)
-      hipLaunchKernelGGL(colsum_vec_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)X, ldx, rows, cols, (float*)ws);
-    else
-      hipLaunchKernelGGL(colsum_vec_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, (float*)ws);
-    CG_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 32)), dim3(256), 0, s, (const float*)ws, nrb, cols,
-                       out, accumulate);
-    CG_LAUNCH_CHECK();
+  int np = 0;
+  const int rc = cg_colsum_partials(dtype, X, ldx, rows > 0 ? rows : 0, cols, (float*)ws, &np, stream);
+  if (rc != CG_OK) return rc;
+  if (np == 0) {  // no rows: the sum is 0
+    if (!accumulate && hipMemsetAsync(out, 0, (size_t)cols * 4, (hipStream_t)stream) != hipSuccess) return CG_ELAUNCH;
     return CG_OK;
   }
-  int nch = COLSUM_R;
-  if (nch > rows) nch = rows > 0 ? rows : 1;
-  dim3 g(cg_cdiv(cols, 256), nch);
-  if (dtype == CG_BF16)
-    hipLaunchKernelGGL(colsum_part_kernel<bf16_t>, g, dim3(256), 0, s, (const bf16_t*)X, ldx, rows, cols, (float*)ws);
-  else
-    hipLaunchKernelGGL(colsum_part_kernel<float>, g, dim3(256), 0, s, (const float*)X, ldx, rows, cols, (float*)ws);
-  CG_LAUNCH_CHECK();
-  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 32)), dim3(256), 0, s, (const float*)ws, nch, cols, out,
-                     accumulate);
+  hipLaunchKernelGGL(colsum_reduce_kernel, dim3(cg_cdiv(cols, 32)), dim3(256), 0, (hipStream_t)stream,
+                     (const float*)ws, np, cols, out, accumulate);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }

@@ -218,6 +218,10 @@ int cg_swiglu_bwd(int dtype, const void* gu, long long ldgu, int Hp, const void*
 size_t cg_colsum_workspace(int rows, int cols);
 int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out,
               int accumulate, void* ws, void* stream);
+/* the first stage alone: *nparts partial rows [*nparts][cols] fp32 into part (sized by
+ * cg_colsum_workspace), for a reduction batched with others (cg_reduce_columns) */
+int cg_colsum_partials(int dtype, const void* X, long long ldx, int rows, int cols, float* part,
+                       int* nparts, void* stream);
 
 /* out[c] (+)= sum_i part[i*cols + c] over nparts partial rows (the second stage of the fused
  * bias-gradient column sums, e.g. CG_EPI_COLSUM GEMM partials) */
