@@ -20,6 +20,7 @@ CG_F32, CG_BF16, CG_BF16X2 = 0, 1, 2
 CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1, 2, 4, 8, 16, 32, 64
 EPI_SWIGLU, EPI_DSWIGLU = 128, 256
+EPI_GELU_DERIV = 512  # GELU: aux_out = gelu'(v); DGELU: aux holds gelu' (out = v * aux)
 (PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV,
  PROBE_GEMM_DW_GROUPED) = range(8)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",

@@ -118,6 +118,13 @@ __device__ __forceinline__ float gelu_fast(float x) {
   float e;
   return x * gelu_phi_q(x, e);
 }
+// gelu(x) and gelu'(x) from one evaluation of Phi and the Gaussian factor
+__device__ __forceinline__ float gelu_fast_d(float x, float& dg) {
+  float e;
+  const float phi = gelu_phi_q(x, e);
+  dg = fmaf(x * 0.39894228040143268f, e, phi);
+  return x * phi;
+}
 __device__ __forceinline__ float dgelu_fast(float x) {
   float e;
   const float phi = gelu_phi_q(x, e);

@@ -691,7 +691,7 @@ int aux_backward(const Ctx& C, int accumulate) {
     CK(defer_colsum(C, dpj, A.ocp[i], C.Lo.off2b[i], accumulate));
     // da = (dpj . W2) * gelu'(a) ; the first Linear's grads
     g = lin_dx(C, dpj, d, C.Lo.off2w[i], d, d, d, da, d);
-    g.epilogue = CG_EPI_DGELU; g.aux = A.oa[i]; g.ld_aux = d;
+    g.epilogue = CG_EPI_DGELU | CG_EPI_GELU_DERIV; g.aux = A.oa[i]; g.ld_aux = d;
     CK(cg_gemm(&g, C.s));
     CK(add_dw(da, A.xf, C.Lo.off1w[i]));
     CK(defer_colsum(C, da, A.ocp[i] + cg_colsum_workspace((int)M, d) / 4, C.Lo.off1b[i], accumulate));
@@ -866,7 +866,7 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     CK(cg_layernorm_fwd(C.dt, a.xmid, d, P(C, o.ln2w), P(C, o.ln2b), a.h2, d, a.mean2, a.rstd2, (int)M, d, eps, C.s));
     if (!D.swiglu) {
       g = lin_fwd(C, a.h2, d, o.w1, d, D.hid, d, a.g, D.hid);
-      g.epilogue = CG_EPI_BIAS | CG_EPI_GELU; g.bias = P(C, o.b1); g.aux_out = a.a; g.ld_aux = D.hid;
+      g.epilogue = CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV; g.bias = P(C, o.b1); g.aux_out = a.a; g.ld_aux = D.hid;
       CK(cg_gemm(&g, C.s));
       g = lin_fwd(C, a.g, D.hid, o.w2, D.hid, d, D.hid, xn, d);
       g.c_dtype = CG_F32;
@@ -934,7 +934,7 @@ extern "C" int cg_model_aux_forward(cg_model* m, float* term_logits, long long l
   for (int i = 0; i < noff; ++i) {
     // offset_projs[k] = Linear -> GELU -> Linear, then the (tied) head
     cg_gemm_desc g = lin_fwd(C, A.xf, d, C.Lo.off1w[i], d, d, d, A.og[i], d);
-    g.epilogue = CG_EPI_BIAS | CG_EPI_GELU; g.bias = P(C, C.Lo.off1b[i]);
+    g.epilogue = CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV; g.bias = P(C, C.Lo.off1b[i]);
     g.aux_out = A.oa[i]; g.ld_aux = d;
     CK(cg_gemm(&g, C.s));
     g = lin_fwd(C, A.og[i], d, C.Lo.off2w[i], d, d, d, A.opj[i], d);
@@ -1018,7 +1018,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       // (b2's gradient was produced by the LayerNorm backward that wrote gin)
       // dGELU product; its fused column sums (64-row partials) are fc1's bias gradient
       cg_gemm_desc g = lin_dx(C, sl.gin, d, o.w2, D.hid, d, D.hid, sl.dmlp, D.hid, a.w2T);
-      g.epilogue = CG_EPI_DGELU | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
+      g.epilogue = CG_EPI_DGELU | CG_EPI_GELU_DERIV | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
       g.workspace = sl.cpart;
       CK(cg_gemm(&g, C.s));
       CK(defer_reduce(m, sl.cpart, D.hid, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
@@ -1255,7 +1255,7 @@ extern "C" int cg_model_decode(cg_model* m, const int64_t* tok, int B, int pos, 
     CK(cg_layernorm_fwd(C.dt, W.xmid, d, P(C, o.ln2w), P(C, o.ln2b), W.h, d, W.mean, W.rstd, B, d, eps, C.s));
     if (!D.swiglu) {
       g = lin_fwd(C, W.h, d, o.w1, d, D.hid, d, W.g, D.hid);
-      g.epilogue = CG_EPI_BIAS | CG_EPI_GELU; g.bias = P(C, o.b1); g.aux_out = W.a; g.ld_aux = D.hid;
+      g.epilogue = CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV; g.bias = P(C, o.b1); g.aux_out = W.a; g.ld_aux = D.hid;
       CK(cg_gemm(&g, C.s));
       g = lin_fwd(C, W.g, D.hid, o.w2, D.hid, d, D.hid, W.x, d);
       g.c_dtype = CG_F32;

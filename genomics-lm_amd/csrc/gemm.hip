@@ -36,13 +36,14 @@ __device__ __forceinline__ void epi_apply(const GemmParams& p, int row, int col,
   if (e & CG_EPI_BIAS) v += p.bias[col];
   const long long ai = (long long)row * p.ld_aux + col;
   if (e & CG_EPI_GELU) {
-    if (p.c_dtype == CG_BF16) ((bf16_t*)p.aux_out)[ai] = f2bf(v);
-    else ((float*)p.aux_out)[ai] = v;
+    const float s = (e & CG_EPI_GELU_DERIV) ? dgelu_f(v) : v;
+    if (p.c_dtype == CG_BF16) ((bf16_t*)p.aux_out)[ai] = f2bf(s);
+    else ((float*)p.aux_out)[ai] = s;
     v = gelu_f(v);
   }
   if (e & CG_EPI_DGELU) {
     float a = (p.c_dtype == CG_BF16) ? bf2f(((const bf16_t*)p.aux)[ai]) : ((const float*)p.aux)[ai];
-    v *= dgelu_f(a);
+    v *= (e & CG_EPI_GELU_DERIV) ? a : dgelu_f(a);
   }
   if (e & CG_EPI_DROPOUT) v = cg_keep(p.drop_seed, (uint32_t)row, (uint32_t)col, p.drop_thr) ? v * p.drop_scale : 0.0f;
   if (e & CG_EPI_RESID) v += p.resid[(long long)row * p.ldr + col];
@@ -265,17 +266,30 @@ __device__ __forceinline__ void epi_apply8(const GemmParams& p, int row, int col
   }
   const long long ai = (long long)row * p.ld_aux + col;
   if (e & CG_EPI_GELU) {
-    if (ct == CG_BF16) st8b((bf16_t*)p.aux_out + ai, v);
-    else st8f((float*)p.aux_out + ai, v);
+    if (e & CG_EPI_GELU_DERIV) {
+      float dg[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_fast(v[j]);
+      for (int j = 0; j < 8; ++j) v[j] = gelu_fast_d(v[j], dg[j]);
+      if (ct == CG_BF16) st8b((bf16_t*)p.aux_out + ai, dg);
+      else st8f((float*)p.aux_out + ai, dg);
+    } else {
+      if (ct == CG_BF16) st8b((bf16_t*)p.aux_out + ai, v);
+      else st8f((float*)p.aux_out + ai, v);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = gelu_fast(v[j]);
+    }
   }
   if (e & CG_EPI_DGELU) {
     float a[8];
     if (ct == CG_BF16) ld8b((const bf16_t*)p.aux + ai, a);
     else ld8f((const float*)p.aux + ai, a);
+    if (e & CG_EPI_GELU_DERIV) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] *= dgelu_fast(a[j]);
+      for (int j = 0; j < 8; ++j) v[j] *= a[j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= dgelu_fast(a[j]);
+    }
   }
   if (e & CG_EPI_DROPOUT) {
 #pragma unroll
@@ -487,6 +501,8 @@ static gemm_kernel_t pick_spec(bool ak, bool bk, int e, int ct) {
   SPEC(true, true, CG_EPI_RESID, CG_F32)
   SPEC(true, true, CG_EPI_DROPOUT | CG_EPI_RESID, CG_F32)
   SPEC(true, true, CG_EPI_DGELU, CG_BF16)
+  SPEC(true, true, CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV, CG_BF16)
+  SPEC(true, true, CG_EPI_DGELU | CG_EPI_GELU_DERIV, CG_BF16)
   SPEC(true, false, 0, CG_BF16)
   SPEC(true, false, 0, CG_F32)
   SPEC(true, false, CG_EPI_DGELU, CG_BF16)
@@ -516,6 +532,9 @@ static gemm_kernel_t pick_pers(int e, int ct) {
   PSPEC(CG_EPI_DGELU, CG_BF16)
   PSPEC(CG_EPI_ACCUM, CG_F32)
   PSPEC(CG_EPI_DGELU | CG_EPI_COLSUM, CG_BF16)
+  PSPEC(CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV, CG_BF16)
+  PSPEC(CG_EPI_DGELU | CG_EPI_GELU_DERIV, CG_BF16)
+  PSPEC(CG_EPI_DGELU | CG_EPI_GELU_DERIV | CG_EPI_COLSUM, CG_BF16)
   PSPEC(CG_EPI_COLSUM, CG_BF16)
   PSPEC(CG_EPI_SWIGLU, CG_BF16)
   PSPEC(CG_EPI_DSWIGLU, CG_BF16)
@@ -620,6 +639,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   if ((p.epi & CG_EPI_RESID) && !p.resid) return CG_EINVAL;
   if ((p.epi & CG_EPI_GELU) && !p.aux_out) return CG_EINVAL;
   if ((p.epi & CG_EPI_DGELU) && !p.aux) return CG_EINVAL;
+  if ((p.epi & CG_EPI_GELU_DERIV) && !(p.epi & (CG_EPI_GELU | CG_EPI_DGELU))) return CG_EINVAL;
   if ((p.epi & CG_EPI_COLSUM) && (!d->workspace || d->split_k > 1)) return CG_EINVAL;
   // SwiGLU epilogues: only the persistent bf16 tile implements them (the caller keeps the
   // separate cg_swiglu_* passes on CG_EUNSUPPORTED)

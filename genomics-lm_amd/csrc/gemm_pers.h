@@ -104,6 +104,15 @@ __device__ __forceinline__ u32x4 pack_bf16(const float v[8]) {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, long long bytes) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
 }
+// sum over each 16-lane row by DPP moves (VALU, no LDS): quad xor 1, quad xor 2, row_half_mirror,
+// row_mirror -- every lane of the row ends with the row's total
+__device__ __forceinline__ float dpp_sum16(float t) {
+  t += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0xB1, 0xF, 0xF, false));
+  t += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x4E, 0xF, 0xF, false));
+  t += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x141, 0xF, 0xF, false));
+  t += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x140, 0xF, 0xF, false));
+  return t;
+}
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -140,13 +149,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     vb[i] = SWG ? b_src_off_swg(pos, p.ldb, p.N) : b_src_off(pos, p.ldb);
   }
 
-  auto tile_org = [&](int k, int& m0, int& n0) {
+  auto tile_org = [&](int k, int& m0, int& n0) __attribute__((always_inline)) {
     const int tile = lb + k * nblk;
     m0 = (tile / tiles_n) * BM;
     n0 = (tile % tiles_n) * BNO;
   };
   // DMA source origins of global k-step g (OOR past the end: the DMA then fills a free slot with zeros)
-  auto stage_org = [&](int g, uint32_t& ao, uint32_t& bo) {
+  auto stage_org = [&](int g, uint32_t& ao, uint32_t& bo) __attribute__((always_inline)) {
     if (g >= S) {
       ao = bo = OOR;
       return;
@@ -157,7 +166,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     ao = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
     bo = (uint32_t)(((long long)n0 * p.ldb + t * BKT) * 2);
   };
-  auto issue = [&](int g) {
+  auto issue = [&](int g) __attribute__((always_inline)) {
     uint32_t ao, bo;
     stage_org(g, ao, bo);
     char* st = smem + (g % STAGES) * STAGE_BYTES;
@@ -176,7 +185,8 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
   int col[2];
   // operand loads of tile k (issued in its last k-step so that the compiler's wait for them in
   // the epilogue does not also wait for the next tile's stage DMAs)
-  auto epi_loads = [&](int k) {
+  auto epi_loads_rows = [&](int k, auto lo_t, auto hi_t, auto bias_t) __attribute__((always_inline)) {
+    constexpr int LO = decltype(lo_t)::value, HI = decltype(hi_t)::value;
     int m0, n0;
     tile_org(k, m0, n0);
     bool cok[2];
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       col[c] = SWG ? n0 + (wn >> 1) + 8 * g4 : n0 + wn + 32 * c + 8 * g4;
       cok[c] = col[c] < p.N;
     }
-    if constexpr ((EPI & CG_EPI_BIAS) != 0) {
+    if constexpr (decltype(bias_t)::value && (EPI & CG_EPI_BIAS) != 0) {
       const __amdgpu_buffer_rsrc_t rbias = rsrc(p.bias, (long long)p.N * 4);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -195,7 +205,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = LO; i < HI; ++i) {
       const int row = m0 + wm + 16 * i + r16;
       const bool rok = row < p.M;
 #pragma unroll
@@ -227,16 +237,17 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       }
     }
   };
+  auto epi_loads = [&](int k) __attribute__((always_inline)) {
+    epi_loads_rows(k, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{}, std::true_type{});
+  };
   v4f acc[4][4];
   // one k-step of global index g (the DMAs of stage g+2 interleaved with the MFMAs, as in the
   // non-persistent 256x128 kernel; they are always issued, so every step carries 6)
   // VMEM ops issued after stage g's DMAs, by position of step g in its tile (k = tile, t = step):
   // stage g+1's DMAs always; the previous tile's epilogue stores when t < 2; its operand loads
   // (issued in its last step, before that step's DMAs) when t == 0
-  auto step = [&](int g, int sel, auto last_tag) {
-    if (sel == 0) wait_vm<DMA_PER_STAGE>();
-    else if (sel == 1) wait_vm<DMA_PER_STAGE + NS>();
-    else wait_vm<DMA_PER_STAGE + NS + NL>();
+  auto step = [&](int g, auto&& wait_fn, auto&& after_fn, auto last_tag) __attribute__((always_inline)) {
+    wait_fn();
     __builtin_amdgcn_s_barrier();
     if constexpr (decltype(last_tag)::value) epi_loads(g / nt);
     const char* st = smem + (g % STAGES) * STAGE_BYTES;
@@ -274,10 +285,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       if (gr < A_CHUNKS + B_CHUNKS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    after_fn();
   };
 
   const bool scaled = p.alpha != 1.0f;
-  auto epilogue = [&](int k) {
+  auto epilogue = [&](int k) __attribute__((always_inline)) {
     int m0, n0;
     tile_org(k, m0, n0);
     float bia[2][8];
@@ -365,21 +377,31 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
         if constexpr ((EPI & CG_EPI_GELU) != 0) {
           const __amdgpu_buffer_rsrc_t rx = rsrc(p.aux_out, ((long long)(p.M - 1) * p.ld_aux + p.N) * ES);
           const uint32_t o = off_c[i][c] == OOR ? OOR : (uint32_t)(((long long)row * p.ld_aux + col[c]) * ES);
-          if constexpr (CT == CG_BF16) {
-            bst(rx, o, pack_bf16(v));
-          } else {
-            bst(rx, o, (u32x4){__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])});
-            bst(rx, o + 16, (u32x4){__float_as_uint(v[4]), __float_as_uint(v[5]), __float_as_uint(v[6]), __float_as_uint(v[7])});
-          }
+          float s[8];  // what aux_out receives: the pre-activation, or gelu' of it
+          if constexpr ((EPI & CG_EPI_GELU_DERIV) != 0) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = gelu_fast(v[j]);
+            for (int j = 0; j < 8; ++j) v[j] = gelu_fast_d(v[j], s[j]);
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s[j] = v[j];
+          }
+          if constexpr (CT == CG_BF16) {
+            bst(rx, o, pack_bf16(s));
+          } else {
+            bst(rx, o, (u32x4){__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])});
+            bst(rx, o + 16, (u32x4){__float_as_uint(s[4]), __float_as_uint(s[5]), __float_as_uint(s[6]), __float_as_uint(s[7])});
+          }
+          if constexpr ((EPI & CG_EPI_GELU_DERIV) == 0) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = gelu_fast(v[j]);
+          }
         }
         if constexpr ((EPI & CG_EPI_DGELU) != 0) {
           float a[8];
           if constexpr (CT == CG_BF16) unpack_bf16(xa[i][c], a);
           else unpack_f32(xa[i][c], xb[i][c], a);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= dgelu_fast(a[j]);
+          for (int j = 0; j < 8; ++j) v[j] *= (EPI & CG_EPI_GELU_DERIV) ? a[j] : dgelu_fast(a[j]);
         }
         if constexpr ((EPI & CG_EPI_DROPOUT) != 0) {
           const uint32_t rh = cg_row_hash(p.drop_seed, (uint32_t)row);
@@ -416,12 +438,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       for (int c = 0; c < 2; ++c)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          float t = csum[c][j];
-          t += __shfl_xor(t, 1, 64);
-          t += __shfl_xor(t, 2, 64);
-          t += __shfl_xor(t, 4, 64);
-          t += __shfl_xor(t, 8, 64);
-          csum[c][j] = t;
+          csum[c][j] = dpp_sum16(csum[c][j]);
         }
       const int prow = (m0 + wm) >> 6;
       const __amdgpu_buffer_rsrc_t rw = rsrc(p.ws, (long long)((p.M + 63) >> 6) * p.N * 4);
@@ -436,18 +453,93 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     }
   };
 
-  issue(0);
-  issue(1);
-  int g = 0;
-  for (int k = 0; k < my_tiles; ++k) {
+  // Epilogue operand loads (NL > 0).  NP == 0: all of them at the top of the tile's last k-step,
+  // before its DMAs.  NP > 0 (nt >= 4): in NP pieces -- piece q loads the lane's row groups
+  // i in [4q/NP, 4(q+1)/NP) (+ the bias with piece 0) -- issued after ALL of step nt-1-NP+q's DMAs
+  // and MFMAs.  A piece then has until the wait of the step three later (which needs the DMAs
+  // issued after it) to land, instead of one k-step, and the loads of all CUs do not arrive as one
+  // burst at the tile's end (C4 dX of fc2 with dGELU: +25 us over the plain product).  Every wait
+  // counts exactly the VMEM ops issued after the stage it needs: the stage after it (6 DMAs) plus
+  // the pieces / epilogue stores issued after each of the two steps before.
+  const auto nopf = [] {};
+  auto tiles = [&](auto np_t) __attribute__((always_inline)) {
+    constexpr int NP = decltype(np_t)::value;
+    constexpr int PI = NP ? (NL - ((EPI & CG_EPI_BIAS) ? 4 : 0)) / 4 : 0;  // ops per row group
+    constexpr int NB = (EPI & CG_EPI_BIAS) ? 4 : 0;
+    // ops of piece x (0 outside [0, NP))
+    constexpr auto pc = [](int x) constexpr {
+      return (x < 0 || x >= NP) ? 0 : PI * (4 * (x + 1) / (NP ? NP : 1) - 4 * x / (NP ? NP : 1)) + (x == 0 ? NB : 0);
+    };
+    constexpr int WL = NP ? pc(NP - 1) : NL;  // ops issued after the last stage of the previous tile
+    issue(0);
+    issue(1);
+    int g = 0;
+    for (int k = 0; k < my_tiles; ++k) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < nt - 1; ++t, ++g) step(g, k > 0 && t < 2 ? (t == 0 ? 2 : 1) : 0, std::false_type{});
-    step(g, k > 0 && nt - 1 < 2 ? 1 : 0, std::true_type{});  // nt >= 2: the last step is never t == 0
-    ++g;
-    epilogue(k);
+        for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+      const int tl = NP ? nt - 1 - NP : nt - 1;  // steps of the runtime loop (NP > 0: >= 2)
+      for (int t = 0; t < tl; ++t, ++g) {
+        const int sel = k > 0 && t < 2 ? (t == 0 ? 2 : 1) : 0;
+        step(
+            g,
+            [&] {
+              if (sel == 0) wait_vm<DMA_PER_STAGE>();
+              else if (sel == 1) wait_vm<DMA_PER_STAGE + NS>();
+              else wait_vm<DMA_PER_STAGE + NS + WL>();
+            },
+            nopf, std::false_type{});
+      }
+      if constexpr (NP == 0) {
+        const int sel = k > 0 && nt - 1 < 2 ? 1 : 0;  // nt >= 2: the last step is never t == 0
+        step(
+            g,
+            [&] {
+              if (sel == 0) wait_vm<DMA_PER_STAGE>();
+              else wait_vm<DMA_PER_STAGE + NS>();
+            },
+            nopf, std::true_type{});
+        ++g;
+      } else {
+        auto tail = [&](auto q_t) __attribute__((always_inline)) {
+          constexpr int Q = decltype(q_t)::value;
+          constexpr int WN = DMA_PER_STAGE + pc(Q - 2) + pc(Q - 1);
+          step(
+              g, [] { wait_vm<WN>(); },
+              [&] {
+                if constexpr (Q < NP) {
+                  __builtin_amdgcn_sched_barrier(0);  // after this step's DMAs, in program order
+                  epi_loads_rows(k, std::integral_constant<int, 4 * Q / NP>{},
+                                 std::integral_constant<int, 4 * (Q + 1) / NP>{}, std::bool_constant<Q == 0>{});
+                }
+              },
+              std::false_type{});
+          ++g;
+        };
+        tail(std::integral_constant<int, 0>{});
+        tail(std::integral_constant<int, 1>{});
+        if constexpr (NP >= 2) tail(std::integral_constant<int, 2>{});
+        if constexpr (NP >= 4) {
+          tail(std::integral_constant<int, 3>{});
+          tail(std::integral_constant<int, 4>{});
+        }
+      }
+      epilogue(k);
+    }
+  };
+#ifndef CG_PERS_NO_SPREAD
+  const int np = NL == 0 ? 0 : nt >= 7 ? 4 : nt >= 5 ? 2 : nt >= 4 ? 1 : 0;
+#else
+  const int np = 0;
+#endif
+  if constexpr (NL == 0 || DSW) {  // DSW: 52 more VGPRs held over 5 steps spill (204 -> 256 + scratch)
+    tiles(std::integral_constant<int, 0>{});
+  } else {
+    if (np == 4) tiles(std::integral_constant<int, 4>{});
+    else if (np == 2) tiles(std::integral_constant<int, 2>{});
+    else if (np == 1) tiles(std::integral_constant<int, 1>{});
+    else tiles(std::integral_constant<int, 0>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
 }

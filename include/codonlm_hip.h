@@ -39,8 +39,11 @@ enum {
   /* SwiGLU (model_tiny_gpt.py:47-57), bf16 persistent tile only (else CG_EUNSUPPORTED): */
   CG_EPI_SWIGLU = 128,   /* B = [w_gate; w_up] (2N rows): aux_out [M][2N] receives the  */
                          /* pre-activations g|u, C [M][N] = silu(g) * u (0 for n >= n_valid) */
-  CG_EPI_DSWIGLU = 256   /* v = dL/ds; aux = g|u [M][2N]: C [M][2N] = d(g|u)             */
+  CG_EPI_DSWIGLU = 256,  /* v = dL/ds; aux = g|u [M][2N]: C [M][2N] = d(g|u)             */
                          /* (0 for n >= n_valid)                                         */
+  CG_EPI_GELU_DERIV = 512 /* modifies GELU / DGELU: the forward's aux_out receives gelu'(v) */
+                         /* instead of v, and the backward's aux holds gelu' (out = v*aux): */
+                         /* the derivative is formed once, from the unrounded pre-activation */
 };
 
 /*

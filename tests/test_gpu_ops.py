@@ -552,11 +552,15 @@ def test_transpose16_batch():
 
 
 @pytest.mark.parametrize("cap", [1, 3])
-@pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256)])
+@pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256), (600, 200, 320),
+                                   (520, 264, 512)])
 def test_gemm_persistent_tile_epilogues(cap, M, N, K):
     """Persistent 256x128 tile (K-contiguous operands): every compile-time epilogue, partial
     M/N tiles, and (cap=3) a grid of 3 workgroups that each walk many tiles, so the LDS-DMA ring
-    and the counted waits carry across tile boundaries with epilogue stores in flight."""
+    and the counted waits carry across tile boundaries with epilogue stores in flight.  K = 128 /
+    192 issue the epilogue loads in the last k-step; K = 256 / 320 / 512 spread them over the
+    tile's last 1 / 2 / 4 k-steps.  CG_EPI_GELU_DERIV: the forward stores gelu'(pre) and the
+    backward multiplies by it."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
     g = torch.Generator().manual_seed(M + N + K)
@@ -586,6 +590,13 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K):
         ops.gemm(xd, wd, out=yac, epilogue=L.EPI_ACCUM, alpha=0.5)
         cs = torch.empty(N, device=DEV)
         ydc = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux, colsum_out=cs)
+        auxd = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        ygd = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV),
+                       epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_DERIV, aux_out=auxd)
+        ydgd = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=auxd)
+        csd = torch.empty(N, device=DEV)
+        ydcd = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=auxd,
+                        colsum_out=csd)
         torch.cuda.synchronize()
     finally:
         L.lib.cg_gemm_set_pers(old)
@@ -606,6 +617,15 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K):
     ref_dg = base * xa.grad
     assert (ydc.float().cpu() - ref_dg).abs().max() < tol + 0.01 * base.abs().max()
     assert (cs.cpu() - ref_dg.sum(0)).abs().max() < 1e-2 * (1 + ref_dg.abs().sum(0).max())
+    # derivative-storing GELU pair
+    xp = pre.clone().requires_grad_(True)
+    F.gelu(xp).sum().backward()
+    assert (auxd.float().cpu() - xp.grad).abs().max() < 0.01 + 0.01 * tol
+    assert (ygd.float().cpu() - F.gelu(pre)).abs().max() < tol + 0.01 * pre.abs().max()
+    ref_dgd = base * auxd.float().cpu()
+    assert (ydgd.float().cpu() - ref_dgd).abs().max() < tol + 0.01 * base.abs().max()
+    assert torch.equal(ydcd.cpu(), ydgd.cpu())
+    assert (csd.cpu() - ref_dgd.sum(0)).abs().max() < 1e-2 * (1 + ref_dgd.abs().sum(0).max())
 
 
 @pytest.mark.parametrize("dtype,pers", [(torch.float32, 1), (torch.bfloat16, 0), (torch.bfloat16, 1)])
