@@ -288,6 +288,102 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     after_fn();
   };
 
+  // Prefetching step (default): the half-0 fragments of step g are read at the END of step g-1 --
+  // after its first eight half-1 MFMAs it waits for stage g's DMAs (its own `vmcnt`, then
+  // lgkmcnt(0) so no wave still reads the slot the next DMAs overwrite), meets the other waves at
+  // the barrier and issues the eight reads under its last eight MFMAs -- so a step starts with
+  // MFMAs instead of LDS latency.  Only a tile's first step syncs at its top (the tile's last
+  // step is followed by the epilogue, which must not hold 32 more registers).  Waits: the top one
+  // as in `step`; the mid one (stage g+1 of step g) counts the ops issued after DMA(g+1): the
+  // pieces / epilogue stores after step g-1 and this step's 6 DMAs.
+#ifndef CG_PERS_NO_PREFETCH
+  // not for the fp32-residual and SwiGLU-backward epilogues: their piece registers plus the
+  // prefetched fragments exceed 256 VGPRs (spills)
+  constexpr bool PREF = !DSW && (EPI & CG_EPI_RESID) == 0;
+#else
+  constexpr bool PREF = false;
+#endif
+  v8bf f0a[4], f0b[4];
+  auto read_half0 = [&](int g) __attribute__((always_inline)) {
+    const char* st = smem + (g % STAGES) * STAGE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f0a[i] = bfg::frag<true>(st, wm + 16 * i, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) f0b[j] = bfrag(st + A_BYTES, wn, j, 0, lane);
+  };
+  auto pstep = [&](int g, bool top, auto&& wait_top, auto mid_tag, auto&& wait_mid, auto&& after_fn,
+                   auto last_tag) __attribute__((always_inline)) {
+    constexpr bool MID = decltype(mid_tag)::value;
+    if (top) {
+      wait_top();
+      __builtin_amdgcn_s_barrier();
+      read_half0(g);
+    }
+    if constexpr (decltype(last_tag)::value) epi_loads(g / nt);
+    const char* st = smem + (g % STAGES) * STAGE_BYTES;
+    const char* as = st;
+    const char* bs = st + A_BYTES;
+    v8bf af1[4], bf1[4];
+    uint32_t ao, bo;
+    stage_org(g + 2, ao, bo);
+    char* nx = smem + ((g + 2) % STAGES) * STAGE_BYTES;
+#pragma unroll
+    for (int gr = 0; gr < 8; ++gr) {
+      const int i = gr >> 1, j0 = 2 * (gr & 1);
+      acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0b[j0], f0a[i], acc[i][j0], 0, 0, 0);
+      acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0b[j0 + 1], f0a[i], acc[i][j0 + 1], 0, 0, 0);
+      if (gr < 4) af1[gr] = bfg::frag<true>(as, wm + 16 * gr, 1, lane);
+      else bf1[gr - 4] = bfrag(bs, wn, gr - 4, 1, lane);
+      if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
+      else if (gr < A_CHUNKS + B_CHUNKS)
+        bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
+    }
+    if constexpr (MID) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int gr = 0; gr < 8; ++gr) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (gr < A_CHUNKS + B_CHUNKS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      wait_mid();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      read_half0(g + 1);
+#pragma unroll
+      for (int i = 2; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int gr = 0; gr < 8; ++gr) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int gr = 0; gr < 8; ++gr) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        if (gr < A_CHUNKS + B_CHUNKS) __builtin_amdgcn_sched_group_barrier(SGB_DMA, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+    }
+    after_fn();
+  };
+
   const bool scaled = p.alpha != 1.0f;
   auto epilogue = [&](int k) __attribute__((always_inline)) {
     int m0, n0;
@@ -480,6 +576,54 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
       const int tl = NP ? nt - 1 - NP : nt - 1;  // steps of the runtime loop (NP > 0: >= 2)
+      if constexpr (PREF) {
+      for (int t = 0; t < tl; ++t, ++g) {
+        const bool top = t == 0;
+        const int sel = k > 0 ? 2 : 0;
+        const bool msel = t == 0 && k > 0;
+        pstep(
+            g, top,
+            [&] {
+              if (sel == 0) wait_vm<DMA_PER_STAGE>();
+              else wait_vm<DMA_PER_STAGE + NS + WL>();
+            },
+            std::true_type{},
+            [&] {
+              if (msel) wait_vm<DMA_PER_STAGE + NS>();
+              else wait_vm<DMA_PER_STAGE>();
+            },
+            nopf, std::false_type{});
+      }
+      if constexpr (NP == 0) {
+        pstep(g, false, nopf, std::false_type{}, nopf, nopf, std::true_type{});
+        ++g;
+      } else {
+        auto tail = [&](auto q_t) __attribute__((always_inline)) {
+          constexpr int Q = decltype(q_t)::value;
+          constexpr int WM = DMA_PER_STAGE + pc(Q - 1);
+          pstep(
+              g, false, nopf, std::bool_constant<(Q < NP)>{}, [] { wait_vm<WM>(); },
+              [&] {
+                if constexpr (Q < NP) {
+                  __builtin_amdgcn_sched_barrier(0);  // after this step's DMAs, in program order
+                  epi_loads_rows(k, std::integral_constant<int, 4 * Q / NP>{},
+                                 std::integral_constant<int, 4 * (Q + 1) / NP>{}, std::bool_constant<Q == 0>{});
+                }
+              },
+              std::false_type{});
+          ++g;
+        };
+        tail(std::integral_constant<int, 0>{});
+        tail(std::integral_constant<int, 1>{});
+        if constexpr (NP >= 2) tail(std::integral_constant<int, 2>{});
+        if constexpr (NP >= 4) {
+          tail(std::integral_constant<int, 3>{});
+          tail(std::integral_constant<int, 4>{});
+        }
+      }
+      epilogue(k);
+      continue;
+      }
       for (int t = 0; t < tl; ++t, ++g) {
         const int sel = k > 0 && t < 2 ? (t == 0 ? 2 : 1) : 0;
         step(
