@@ -301,41 +301,57 @@ static bool ln_bwd_fast(int W, int cols, int nblk, hipStream_t s, const TD* dy, 
 #undef LNB
 }
 
-// sum the per-block partial rows: 16 columns x 64 row lanes per block, 4 independent chains per
-// lane (16 loads in flight at nblk = 1024), fixed summation order
+// Column sums of a [nrows][ld] fp32 partial-row block for the 32 columns c0 .. c0+31, one
+// 1024-thread block, in a fixed order: row lane v in [0, 64) sums rows v + 64u + 256k in 4 chains
+// u (the tail rows into chain 0), the chains combine as (0+1)+(2+3), the lanes in 8 groups of 8,
+// then the 8 group sums.  Thread (tx, ty) serves lanes ty and ty + 32 of column c0 + tx, so every
+// wave load covers two 128-B row segments.  The result is valid in threads ty == 0.
+__device__ __forceinline__ float colred32(const float* __restrict__ part, long long ld, int nrows, int ncols, int c0,
+                                          float (*red)[33]) {
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int c = c0 + tx;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int v = ty + 32 * h;
+    float s = 0.f;
+    if (c < ncols) {
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      int b = v;
+      for (; b + 192 < nrows; b += 256)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s4[u] += part[(long long)(b + 64 * u) * ld + c];
+      for (; b < nrows; b += 64) s4[0] += part[(long long)b * ld + c];
+      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    }
+    red[v][tx] = s;
+  }
+  __syncthreads();
+  float g = 0.f;
+  if (ty < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) g += red[ty * 8 + i][tx];
+  }
+  __syncthreads();
+  if (ty < 8) red[ty][tx] = g;
+  __syncthreads();
+  float t = 0.f;
+  if (ty == 0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += red[i][tx];
+  }
+  return t;
+}
+
+// sum the per-block partial rows of the LayerNorm backward (colred32 order)
 // (nw = 2: dgamma|dbeta, nw = 3: dgamma|dbeta|dcol)
 __global__ __launch_bounds__(1024) void ln_param_reduce2(const float* __restrict__ partials, int nblk, int cols,
                                                          int nw, float* __restrict__ dgamma,
                                                          float* __restrict__ dbeta, float* __restrict__ dcol,
                                                          int accumulate) {
-  __shared__ float red[64][17];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int c = blockIdx.x * 16 + tx;
-  const long long ld = (long long)nw * cols;
-  float s = 0.f;
-  if (c < nw * cols) {
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};
-    int b = ty;
-    for (; b + 192 < nblk; b += 256)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) s4[u] += partials[(long long)(b + 64 * u) * ld + c];
-    for (; b < nblk; b += 64) s4[0] += partials[(long long)b * ld + c];
-    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-  }
-  red[ty][tx] = s;
-  __syncthreads();
-  float v = 0.f;
-  if (ty < 8) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v += red[ty * 8 + i][tx];
-  }
-  __syncthreads();
-  if (ty < 8) red[ty][tx] = v;
-  __syncthreads();
-  if (ty == 0 && c < nw * cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t += red[i][tx];
+  __shared__ float red[64][33];
+  const int c = blockIdx.x * 32 + (threadIdx.x & 31);
+  const float t = colred32(partials, (long long)nw * cols, nblk, nw * cols, blockIdx.x * 32, red);
+  if ((threadIdx.x >> 5) == 0 && c < nw * cols) {
     float* dst = c < cols ? dgamma + c : c < 2 * cols ? dbeta + (c - cols) : dcol + (c - 2 * cols);
     *dst = accumulate ? *dst + t : t;
   }
@@ -497,7 +513,7 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
   if (rc != CG_OK) return rc;
   if (dgamma && dbeta) {
     if (fast)
-      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 16)), dim3(1024), 0, s, partials, nblk,
+      hipLaunchKernelGGL(ln_param_reduce2, dim3(cg_cdiv((2 + want_col) * cols, 32)), dim3(1024), 0, s, partials, nblk,
                          cols, 2 + want_col, dgamma, dbeta, dcolsum, accumulate);
     else
       hipLaunchKernelGGL(ln_param_reduce_kernel, dim3(cg_cdiv((2 + want_col) * cols, 256)), dim3(256), 0, s, partials,
@@ -519,43 +535,17 @@ extern "C" int cg_layernorm_bwd_partials(int dy_dtype, const void* dy, long long
                      partials, want_col ? 1 : 0, rows, cols, (hipStream_t)stream, &fast);
 }
 
-// Batched column reductions (cg_reduce_columns): one 1024-thread block = 16 columns x 64 row
-// lanes of one job, 4 independent chains per lane, the same fixed order as ln_param_reduce2 (so a
-// deferred LayerNorm reduction is bitwise the in-call one); the block finds its job by a scan
-// over the (<= CG_REDUCE_MAX) first-block offsets
+// Batched column reductions (cg_reduce_columns): one 1024-thread block = 32 columns of one job in
+// the colred32 order (the order of ln_param_reduce2, so a deferred LayerNorm reduction is bitwise
+// the in-call one); the block finds its job by a scan over the (<= CG_REDUCE_MAX) first-block offsets
 __global__ __launch_bounds__(1024) void reduce_columns_kernel(cg_reduce_batch bt) {
-  __shared__ float red[64][17];
+  __shared__ float red[64][33];
   int j = 0;
   while (j + 1 < bt.n && bt.j[j + 1].first_block <= (int)blockIdx.x) ++j;
   const cg_reduce_job& jb = bt.j[j];
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  const int c = ((int)blockIdx.x - jb.first_block) * 16 + tx;
-  float s = 0.f;
-  if (c < jb.cols) {
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};
-    int b = ty;
-    for (; b + 192 < jb.nrows; b += 256)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) s4[u] += jb.part[(long long)(b + 64 * u) * jb.ld + c];
-    for (; b < jb.nrows; b += 64) s4[0] += jb.part[(long long)b * jb.ld + c];
-    s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-  }
-  red[ty][tx] = s;
-  __syncthreads();
-  float v = 0.f;
-  if (ty < 8) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v += red[ty * 8 + i][tx];
-  }
-  __syncthreads();
-  if (ty < 8) red[ty][tx] = v;
-  __syncthreads();
-  if (ty == 0 && c < jb.cols) {
-    float t = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) t += red[i][tx];
-    jb.dst[c] = jb.accumulate ? jb.dst[c] + t : t;
-  }
+  const int c0 = ((int)blockIdx.x - jb.first_block) * 32, c = c0 + (threadIdx.x & 31);
+  const float t = colred32(jb.part, jb.ld, jb.nrows, jb.cols, c0, red);
+  if ((threadIdx.x >> 5) == 0 && c < jb.cols) jb.dst[c] = jb.accumulate ? jb.dst[c] + t : t;
 }
 
 extern "C" int cg_reduce_columns(const cg_reduce_batch* batch, void* stream) {
@@ -568,7 +558,7 @@ extern "C" int cg_reduce_columns(const cg_reduce_batch* batch, void* stream) {
     if (q.cols == 0) continue;
     bt.j[k] = q;
     bt.j[k].first_block = nb;
-    nb += cg_cdiv(q.cols, 16);
+    nb += cg_cdiv(q.cols, 32);
     ++k;
   }
   bt.n = k;
