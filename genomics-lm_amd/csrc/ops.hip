@@ -224,6 +224,13 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
     const TD* dyr = dy + (long long)row * lddy;
     float xh[NV][W], gy[NV][W];
     float s1 = 0.f, s2 = 0.f;
+    // the residual-gradient row is loaded with dy and x, before the two row reductions
+    const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
+    float g2[NV][W];
+    if (gi) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) ldw<W>(gi + W * (lane + 64 * i), g2[i]);
+    }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = W * (lane + 64 * i);
@@ -243,7 +250,6 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
     s1 = wave_sum(s1) * (1.0f / cols);
     s2 = wave_sum(s2) * (1.0f / cols);
     float* go = g_out + (long long)row * cols;
-    const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = W * (lane + 64 * i);
@@ -251,10 +257,8 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
 #pragma unroll
       for (int j = 0; j < W; ++j) o[j] = rs * (gy[i][j] - s1 - xh[i][j] * s2);
       if (gi) {
-        float g2[W];
-        ldw<W>(gi + c, g2);
 #pragma unroll
-        for (int j = 0; j < W; ++j) o[j] += g2[j];
+        for (int j = 0; j < W; ++j) o[j] += g2[i][j];
       }
       stw<W>(go + c, o);
       if (g_out_t) {
