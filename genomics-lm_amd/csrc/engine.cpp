@@ -323,7 +323,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   // also holds the fused bias-gradient column-sum partials ([ceil(M/64)][cols])
   A.splitws_floats = std::max<size_t>(A.splitws_floats, (size_t)((M + 63) / 64) * (size_t)big);
   A.splitws = w.take<float>(A.splitws_floats * 4);
-  A.embws = w.take<float>((size_t)32 * D.V * d * 4);
+  A.embws = w.take<float>(cg_embed_bwd_workspace((int)B, (int)T, D.V, d));  // bytes, sized by the kernel's own chunking
   A.cews = w.take<float>(cg_ce_workspace((int)M));
   static const bool wt_env = [] { const char* e = getenv("CG_DX_TRANSPOSE"); return !e || atoi(e) != 0; }();
   A.wT = wt_env && c->dtype == CG_BF16 && d % 8 == 0 && D.Nqkv % 8 == 0 && D.hid % 8 == 0 && D.Hp % 8 == 0;
