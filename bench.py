@@ -275,14 +275,14 @@ def main():
     dominant = 0
     if not args.no_kernel_roofline and args.dtype == "bf16":
         nxt = args.warmup
-        for kind in (L.PROBE_GEMM_DW_GROUPED, L.PROBE_GEMM_DW, L.PROBE_GEMM_FWD, L.PROBE_GEMM_DX, L.PROBE_ATTN_FWD,
-                     L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV):
+        for kind in (L.PROBE_GEMM_PERS, L.PROBE_GEMM_DW_GROUPED, L.PROBE_GEMM_DW, L.PROBE_GEMM_FWD, L.PROBE_GEMM_DX,
+                     L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV):
             probes[kind] = probe_pass(kind, run, nxt, 2)
             nxt += 2
-        # roofline candidates are single kernels (one rocprof row each); the fwd/dX GEMM classes
-        # span several epilogue specialisations and are reported under "kernels" only
-        single = tuple(L.PROBE_KERNELS)
-        dominant = max(single, key=lambda k: probes[k][1])
+        # the roofline kernel is the MFMA kernel class with the most device time per step (a class =
+        # one kernel template: the persistent fwd/dX GEMM with all its epilogue instantiations, the
+        # grouped dW with its tile variants, each attention kernel)
+        dominant = max(tuple(L.PROBE_KERNELS), key=lambda k: probes[k][1])
         if world > 1:  # all ranks probe the same kernel in the timed region
             t = torch.tensor([dominant], device=dev)
             dist.broadcast(t, 0)
@@ -290,8 +290,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # live HIP events around that kernel's launches in the timed region, 1 launch in 4
-    L.lib.cg_probe_sample(4)
+    # live HIP events around that class's launches in the timed region, 1 launch in `every`: the
+    # smallest every >= 4 coprime to the class's launches per step, so over the timed steps the
+    # sampled launches cycle through every product of the step (a class spans several shapes)
+    per_step = max(1, probes[dominant][2] // 2) if dominant else 1
+    every = next(e for e in range(4, 64) if math.gcd(e, per_step) == 1)
+    L.lib.cg_probe_sample(every)
     L.lib.cg_probe_enable(dominant)
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -306,8 +310,10 @@ def main():
         import ctypes as C
         w, ms, k = C.c_double(0), C.c_double(0), C.c_longlong(0)
         L.check(L.lib.cg_probe_read(C.byref(w), C.byref(ms), C.byref(k)), "cg_probe_read")
+        nbytes = C.c_double(0)
+        L.check(L.lib.cg_probe_bytes(C.byref(nbytes)), "cg_probe_bytes")
         L.lib.cg_probe_enable(0)
-        live = (w.value, ms.value, k.value)
+        live = (w.value, ms.value, k.value, nbytes.value)
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -349,27 +355,39 @@ def main():
         "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),
     }
     if rank == 0 and live is not None and live[1] > 0:
-        work, ms, k = live
+        work, ms, k, abytes = live
         ach = work / (ms * 1e-3) / 1e12
-        result["roofline"] = {"kernel": L.PROBE_NAMES[dominant], "bound": "mfma", "achieved": round(ach, 2),
+        result["roofline"] = {"kernel": L.PROBE_NAMES[dominant], "rocprof_kernels": L.PROBE_KERNELS[dominant] + "*",
+                              "bound": "mfma", "achieved": round(ach, 2),
                               "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                               "traffic": None, "launches": k, "avg_launch_us": round(ms / k * 1e3, 2),
-                              "measured": "HIP events on the launch stream around 1 in 4 launches of the kernel in "
-                                          "the timed region"}
-        # HBM bytes per launch of the same kernel from the committed rocprofv3 PMC passes
-        # (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections); attached only for the same config,
-        # batch and kernel, with the commit the counters were collected at
-        tr = ROOT / "profiles" / "round2" / f"pmc_traffic_{args.config}.json"
-        if tr.exists() and B == CONFIGS[args.config]["batch"]:
+                              "ms_per_step_probe": round(probes[dominant][1] / 2, 3),
+                              "algorithmic_bytes_per_launch": round(abytes / k) if k else None,
+                              "measured": f"HIP events on the launch stream around 1 in {every} launches of the "
+                                          f"kernel class ({per_step} launches per step) in the timed region; "
+                                          "achieved = sum of their algorithmic FLOPs (2MNK) / sum of their device time"}
+        # HBM bytes per launch of the same kernel class from the committed rocprofv3 PMC passes
+        # (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections; tools/pmc_traffic.py); attached only for
+        # the same config, batch and kernel class, newest round first, with the commit the counters
+        # were collected at
+        name = L.PROBE_NAMES[dominant]
+        cands = sorted(ROOT.glob(f"profiles/round*/pmc_traffic_{args.config}_{name}.json"), reverse=True)
+        cands += [ROOT / "profiles" / "round2" / f"pmc_traffic_{args.config}.json"]
+        for tr in cands:
+            if not tr.exists() or B != CONFIGS[args.config]["batch"]:
+                continue
             t = json.loads(tr.read_text())
-            if t.get("probe") == L.PROBE_NAMES[dominant]:
-                result["roofline"]["traffic"] = t["hbm_bytes_per_launch"]
-                result["roofline"]["traffic_unit"] = "HBM bytes/launch (PMC)"
-                result["roofline"]["traffic_source"] = (f"profiles/round2/pmc_traffic_{args.config}.json "
-                                                        f"(collected at {t.get('commit')}; this run {_head()})")
-                result["roofline"]["traffic_algorithmic"] = t.get("algorithmic_bytes_per_launch")
+            if t.get("probe") != name:
+                continue
+            result["roofline"]["traffic"] = t["hbm_bytes_per_launch"]
+            result["roofline"]["traffic_unit"] = "HBM bytes/launch (PMC)"
+            result["roofline"]["traffic_source"] = (f"{tr.relative_to(ROOT)} "
+                                                    f"(collected at {t.get('commit')}; this run {_head()})")
+            result["roofline"]["traffic_algorithmic"] = t.get("algorithmic_bytes_per_launch")
+            break
         result["kernels"] = {
             L.PROBE_NAMES[kk]: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None,
+                                "frac": round(v[0] / (v[1] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4) if v[1] > 0 else None,
                                 "ms_per_step": round(v[1] / 2, 3), "launches_per_step": v[2] // 2}
             for kk, v in probes.items() if v[2]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

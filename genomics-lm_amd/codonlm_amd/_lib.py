@@ -22,13 +22,16 @@ EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1
 EPI_SWIGLU, EPI_DSWIGLU = 128, 256
 EPI_GELU_DERIV = 512  # GELU: aux_out = gelu'(v); DGELU: aux holds gelu' (out = v * aux)
 (PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV,
- PROBE_GEMM_DW_GROUPED) = range(8)
+ PROBE_GEMM_DW_GROUPED, PROBE_GEMM_PERS) = range(9)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
                PROBE_ATTN_FWD: "attn_fwd_mfma", PROBE_ATTN_DQ: "attn_bwd_dq_mfma",
-               PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma", PROBE_GEMM_DW_GROUPED: "gemm_dw_grouped"}
-# rocprofv3 kernel-name prefixes of the probed kernels (bench.py matches profiles against them)
+               PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma", PROBE_GEMM_DW_GROUPED: "gemm_dw_grouped",
+               PROBE_GEMM_PERS: "gemm_bf16_pers"}
+# rocprofv3 kernel-name prefixes of the probed kernel classes (every instantiation whose name
+# starts with the prefix belongs to the class; bench.py / tools/kstats.py sum them)
 PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: "gemm_dw_kernel", PROBE_ATTN_FWD: "attn_fwd_mfma",
-                 PROBE_ATTN_DQ: "attn_bwd_dq_mfma", PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma"}
+                 PROBE_ATTN_DQ: "attn_bwd_dq_mfma", PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma",
+                 PROBE_GEMM_PERS: "gemm_bf16_pers_kernel"}
 
 # parameter kinds (enum in the header)
 (P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,
@@ -47,7 +50,7 @@ class GemmDesc(C.Structure):
                 ("bias", vp), ("resid", vp), ("ldr", i64),
                 ("aux", vp), ("aux_out", vp), ("ld_aux", i64),
                 ("drop_seed", u32), ("drop_p", f32), ("split_k", i32), ("workspace", vp),
-                ("n_valid", i32)]
+                ("n_valid", i32), ("ws_bytes", sz)]
 
 
 DW_MAX = 32
@@ -122,14 +125,15 @@ SIGNATURES = {
     "cg_gemm_dw_set_tile": (i32, [i32]),
     "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
     "cg_layernorm_bwd_blocks": (i32, [i32]),
-    "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, vp, vp,
+    "cg_layernorm_bwd_workspace": (sz, [i32, i32, i32]),
+    "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, sz, vp, vp,
                                vp, i32, i32, i32, f32, vp]),
-    "cg_layernorm_bwd_partials": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, i32,
+    "cg_layernorm_bwd_partials": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, sz, i32,
                                         i32, i32, vp]),
     "cg_reduce_columns": (i32, [C.POINTER(ReduceBatch), vp]),
     "cg_embed_fwd": (i32, [vp, vp, vp, vp, i32, i32, i32, u32, f32, vp]),
     "cg_embed_bwd_workspace": (sz, [i32, i32, i32, i32]),
-    "cg_embed_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, u32, f32, i32, vp, vp]),
+    "cg_embed_bwd": (i32, [vp, vp, vp, vp, i32, i32, i32, i32, u32, f32, i32, vp, sz, vp]),
     "cg_segment_starts": (i32, [vp, vp, i32, i32, i32, vp]),
     "cg_rope_tab": (i32, [i32, vp, i64, i32, i32, i32, i32, i32, vp, vp, i32, vp]),
     "cg_attn_fwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp, vp]),
@@ -138,15 +142,15 @@ SIGNATURES = {
     "cg_attn_probs": (i32, [i32, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
-                          u32, f32, vp, vp, i64, vp, vp]),
+                          u32, f32, vp, vp, i64, vp, sz, vp]),
     "cg_ce_workspace": (sz, [i32]),
-    "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, vp]),
+    "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, sz, vp]),
     "cg_swiglu_fwd": (i32, [i32, vp, i64, i32, vp, i64, i32, i32, vp]),
     "cg_swiglu_bwd": (i32, [i32, vp, i64, i32, vp, i64, vp, i64, i32, i32, vp]),
     "cg_colsum_workspace": (sz, [i32, i32]),
-    "cg_colsum": (i32, [i32, vp, i64, i32, i32, vp, i32, vp, vp]),
+    "cg_colsum": (i32, [i32, vp, i64, i32, i32, vp, i32, vp, sz, vp]),
     "cg_colsum_reduce": (i32, [vp, i32, i32, vp, i32, vp]),
-    "cg_colsum_partials": (i32, [i32, vp, i64, i32, i32, vp, C.POINTER(i32), vp]),
+    "cg_colsum_partials": (i32, [i32, vp, i64, i32, i32, vp, sz, C.POINTER(i32), vp]),
     "cg_cast_f32_to_bf16": (i32, [vp, vp, i64, vp]),
     "cg_transpose16_batch": (i32, [C.POINTER(TransposeBatch), vp]),
     "cg_cast_bf16_to_f32": (i32, [vp, vp, i64, vp]),
@@ -176,6 +180,7 @@ SIGNATURES = {
     "cg_probe_enable": (i32, [i32]),
     "cg_probe_sample": (i32, [i32]),
     "cg_probe_read": (i32, [C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(i64)]),
+    "cg_probe_bytes": (i32, [C.POINTER(C.c_double)]),
     "cg_version": (C.c_char_p, []),
 }
 

@@ -68,6 +68,7 @@ def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=No
     d.ld_aux = aux_t.stride(0) if aux_t is not None else 0
     d.drop_seed, d.drop_p = int(drop_seed) & 0xFFFFFFFF, float(drop_p)
     d.split_k, d.workspace = int(split_k), _p(ws)
+    d.ws_bytes = 0 if ws is None else ws.numel() * ws.element_size()
     d.n_valid = int(n_valid)
     L.check(L.lib.cg_gemm(C.byref(d), L.stream_ptr(a.device)), "cg_gemm")
     if colsum_out is not None:
@@ -94,8 +95,8 @@ def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5, branch_dtype=N
     (g_out, dgamma, dbeta, g_branch, colsum); else (g_out, dgamma, dbeta)."""
     rows, cols = x.shape
     g_out = torch.empty(rows, cols, dtype=torch.float32, device=x.device)
-    nblk = L.lib.cg_layernorm_bwd_blocks(rows)
-    part = torch.empty(nblk * 3 * cols, dtype=torch.float32, device=x.device)
+    part_bytes = int(L.lib.cg_layernorm_bwd_workspace(rows, cols, 1))
+    part = torch.empty(max(1, part_bytes // 4), dtype=torch.float32, device=x.device)
     dgamma = torch.empty(cols, dtype=torch.float32, device=x.device)
     dbeta = torch.empty_like(dgamma)
     branch = colsum = None
@@ -105,7 +106,8 @@ def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5, branch_dtype=N
     L.check(L.lib.cg_layernorm_bwd(_dt(dy), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), mean.data_ptr(),
                                    rstd.data_ptr(), weight.data_ptr(), _p(g_in), g_out.data_ptr(),
                                    _dt(branch) if branch is not None else L.CG_F32, _p(branch), drop_seed, drop_p,
-                                   part.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), _p(colsum), 0, rows, cols,
+                                   part.data_ptr(), part_bytes, dgamma.data_ptr(), dbeta.data_ptr(), _p(colsum), 0,
+                                   rows, cols,
                                    eps, L.stream_ptr(x.device)), "cg_layernorm_bwd")
     if branch_dtype is not None:
         return g_out, dgamma, dbeta, branch, colsum
@@ -124,7 +126,8 @@ def layernorm_bwd_partials(dy, x, mean, rstd, weight, g_in=None, branch_dtype=No
     L.check(L.lib.cg_layernorm_bwd_partials(_dt(dy), dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0),
                                             mean.data_ptr(), rstd.data_ptr(), weight.data_ptr(), _p(g_in),
                                             g_out.data_ptr(), _dt(branch) if branch is not None else L.CG_F32,
-                                            _p(branch), drop_seed, drop_p, part.data_ptr(), int(nw == 3), rows, cols,
+                                            _p(branch), drop_seed, drop_p, part.data_ptr(),
+                                            part.numel() * 4, int(nw == 3), rows, cols,
                                             L.stream_ptr(x.device)), "cg_layernorm_bwd_partials")
     return g_out, part, branch
 
@@ -206,7 +209,7 @@ def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, 
                               dy.data_ptr(), dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), B, T, H,
                               KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF, float(drop_p), _p(drop_mask),
                               _p(bias_part), 0 if bias_part is None else bias_part.stride(0),
-                              ws.data_ptr(), L.stream_ptr(qkv.device)), "cg_attn_bwd")
+                              ws.data_ptr(), ws.numel() * 4, L.stream_ptr(qkv.device)), "cg_attn_bwd")
     return dqkv
 
 
@@ -218,7 +221,8 @@ def cross_entropy(logits, targets, eps=0.0, weight=None, ignore_index=0, grad_dt
     ws = torch.empty(int(L.lib.cg_ce_workspace(rows)) // 4 + 1, dtype=torch.float32, device=logits.device)
     L.check(L.lib.cg_cross_entropy(logits.data_ptr(), logits.stride(0), targets.contiguous().data_ptr(), rows, V,
                                    float(eps), _p(weight), int(ignore_index), 1.0, _dt(dl), dl.data_ptr(), ldd,
-                                   loss.data_ptr(), ws.data_ptr(), L.stream_ptr(logits.device)), "cg_cross_entropy")
+                                   loss.data_ptr(), ws.data_ptr(), ws.numel() * 4, L.stream_ptr(logits.device)),
+            "cg_cross_entropy")
     return loss, dl
 
 
@@ -314,7 +318,7 @@ def colsum(x, out=None, accumulate=False):
         out = torch.empty(cols, dtype=torch.float32, device=x.device)
     ws = torch.empty(int(L.lib.cg_colsum_workspace(rows, cols)) // 4 + 1, dtype=torch.float32, device=x.device)
     L.check(L.lib.cg_colsum(_dt(x), x.data_ptr(), x.stride(0), rows, cols, out.data_ptr(), int(bool(accumulate)),
-                            ws.data_ptr(), L.stream_ptr(x.device)), "cg_colsum")
+                            ws.data_ptr(), ws.numel() * 4, L.stream_ptr(x.device)), "cg_colsum")
     return out
 
 

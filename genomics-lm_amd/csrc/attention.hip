@@ -380,8 +380,9 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
                            long long ldy, const void* dy, long long lddy, const float* lse, void* dqkv,
                            long long lddqkv, int B, int T, int H, int KV, int hd, int window, uint32_t drop_seed,
                            float drop_p, const void* drop_mask, float* bias_part, long long ld_part, void* ws,
-                           void* stream) {
+                           size_t ws_bytes, void* stream) {
   if (KV <= 0 || H % KV) return CG_EINVAL;
+  if (B > 0 && T > 0 && (!ws || ws_bytes < cg_attn_bwd_workspace(B, T, H))) return CG_EINVAL;
   if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
   if (B == 0 || T == 0) return CG_OK;
   hipStream_t s = (hipStream_t)stream;

@@ -216,6 +216,10 @@ struct DwSlot {
   // dbeta | consumer bias), fc1 bias ([ceil(M/64)][hid]), qkv bias ([B*ceil(T/128)][Nqkv])
   float *lnp2, *lnp1, *cpart, *bpart;
 };
+// byte sizes of the carved scratch buffers handed to the op entry points (their ws_bytes)
+struct WsBytes {
+  size_t lnp, cpart, colws, splitws, embws, cews, delta, ocp_half;
+};
 struct Acts {
   int32_t* seg;
   std::vector<DwSlot> slot;
@@ -230,6 +234,7 @@ struct Acts {
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
   float* bpart;  // qkv bias-gradient partials from the attention backward [B*ceil(T/128)][Nqkv]
   size_t splitws_floats;
+  WsBytes nb;
   bool wT;  // transposed weight copies present
   // auxiliary offset heads: pre-GELU a, GELU output g, projection pj (compute dtype, M x d)
   std::vector<void*> oa, og, opj;
@@ -284,8 +289,9 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   const long long ldl_ = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
   char* opj_all = noff ? w.take<char>((size_t)noff * M * d * es) : nullptr;
   char* odl_all = noff ? w.take<char>((size_t)noff * M * ldl_ * es_dl) : nullptr;
+  A.nb.ocp_half = cg_colsum_workspace((int)M, d);
   for (int i = 0; i < noff; ++i) {
-    A.ocp[i] = w.take<float>(2 * cg_colsum_workspace((int)M, d));
+    A.ocp[i] = w.take<float>(2 * A.nb.ocp_half);
     A.opj[i] = opj_all + (size_t)i * M * d * es;
     A.odl[i] = odl_all + (size_t)i * M * ldl_ * es_dl;
     A.odpj[i] = w.take<char>(M * d * es);
@@ -296,14 +302,16 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.ldl = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
   A.dlogits = w.take<char>(M * A.ldl * es);
   A.slot.resize(D.G);
+  A.nb.lnp = cg_layernorm_bwd_workspace((int)M, d, 1);
+  A.nb.cpart = (size_t)((M + 63) / 64) * std::max(D.hid, d) * 4;
   for (auto& sl : A.slot) {
     sl.gin = w.take<char>(M * d * es);
     sl.gattn = w.take<char>(M * d * es);
     sl.dmlp = w.take<char>(M * (D.swiglu ? 2LL * D.Hp : (long long)D.hid) * es);
     sl.dqkv = w.take<char>(M * D.Nqkv * es);
-    sl.lnp2 = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
-    sl.lnp1 = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
-    sl.cpart = w.take<float>((size_t)((M + 63) / 64) * std::max(D.hid, d) * 4);
+    sl.lnp2 = w.take<float>(A.nb.lnp);
+    sl.lnp1 = w.take<float>(A.nb.lnp);
+    sl.cpart = w.take<float>(A.nb.cpart);
     sl.bpart = w.take<float>((size_t)B * ((T + 127) / 128) * D.Nqkv * 4);
   }
   A.head2 = c->dtype == CG_BF16 ? w.take<char>((size_t)2 * D.Vp * d * 2) : nullptr;
@@ -312,19 +320,24 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.dsmall = w.take<char>(M * std::max(d, D.Hp) * es);
   A.g = w.take<float>(M * d * 4);
   A.dtmp = w.take<float>(M * d * 4);
-  A.delta = w.take<float>((size_t)B * D.H * T * 4);
-  A.lnpart = w.take<float>((size_t)cg_layernorm_bwd_blocks((int)M) * 3 * d * 4);
+  A.nb.delta = cg_attn_bwd_workspace(B, T, D.H);
+  A.delta = w.take<float>(A.nb.delta);
+  A.lnpart = w.take<float>(A.nb.lnp);
   const long long maxcols = std::max<long long>({big, (long long)d, (long long)D.Hp});
-  A.colws = w.take<float>(cg_colsum_workspace((int)M, (int)maxcols));
+  A.nb.colws = cg_colsum_workspace((int)M, (int)maxcols);
+  A.colws = w.take<float>(A.nb.colws);
   A.bpart = w.take<float>((size_t)B * ((T + 127) / 128) * D.Nqkv * 4);
   long long wmax = std::max<long long>({(long long)D.Nqkv * d, (long long)D.hid * d, 2LL * D.Hp * d,
                                         (long long)D.Vp * d, (long long)d * d});
   A.splitws_floats = (size_t)MAX_SPLIT * wmax;
   // also holds the fused bias-gradient column-sum partials ([ceil(M/64)][cols])
   A.splitws_floats = std::max<size_t>(A.splitws_floats, (size_t)((M + 63) / 64) * (size_t)big);
-  A.splitws = w.take<float>(A.splitws_floats * 4);
-  A.embws = w.take<float>(cg_embed_bwd_workspace((int)B, (int)T, D.V, d));  // bytes, sized by the kernel's own chunking
-  A.cews = w.take<float>(cg_ce_workspace((int)M));
+  A.nb.splitws = A.splitws_floats * 4;
+  A.splitws = w.take<float>(A.nb.splitws);
+  A.nb.embws = cg_embed_bwd_workspace((int)B, (int)T, D.V, d);  // bytes, sized by the kernel's own chunking
+  A.embws = w.take<float>(A.nb.embws);
+  A.nb.cews = cg_ce_workspace((int)M);
+  A.cews = w.take<float>(A.nb.cews);
   static const bool wt_env = [] { const char* e = getenv("CG_DX_TRANSPOSE"); return !e || atoi(e) != 0; }();
   A.wT = wt_env && c->dtype == CG_BF16 && d % 8 == 0 && D.Nqkv % 8 == 0 && D.hid % 8 == 0 && D.Hp % 8 == 0;
   for (int l = 0; l < D.L; ++l) {
@@ -504,10 +517,11 @@ int lin_dw(const Ctx& C, const void* dy, long long lddy, const void* x, long lon
   g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
   g.split_k = pick_split(C, N, K, C.M);
   g.workspace = C.A.splitws;
+  g.ws_bytes = C.A.nb.splitws;
   return cg_gemm(&g, C.s);
 }
 int bias_grad(const Ctx& C, const void* dy, long long lddy, int N, long long goff, int accumulate) {
-  return cg_colsum(C.dt, dy, lddy, (int)C.M, N, G(C, goff), accumulate, C.A.colws, C.s);
+  return cg_colsum(C.dt, dy, lddy, (int)C.M, N, G(C, goff), accumulate, C.A.colws, C.A.nb.colws, C.s);
 }
 
 float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
@@ -556,7 +570,7 @@ int ln_bwd_deferred(const Ctx& C, int dy_dtype, const void* dy, const float* x, 
                     float* dbeta, float* dcol, int accumulate) {
   const int d = C.D.d;
   CK(cg_layernorm_bwd_partials(dy_dtype, dy, d, x, d, mean, rstd, P(C, gw), g_in, C.A.g, C.dt, g_out_t, seed, p, part,
-                               dcol ? 1 : 0, (int)C.M, d, C.s));
+                               C.A.nb.lnp, dcol ? 1 : 0, (int)C.M, d, C.s));
   const int nw = dcol ? 3 : 2;
   const int nblk = cg_layernorm_bwd_blocks((int)C.M);
   CK(defer_reduce(C.m, part, (long long)nw * d, nblk, d, dgamma, accumulate, C.s));
@@ -568,7 +582,7 @@ int ln_bwd_deferred(const Ctx& C, int dy_dtype, const void* dy, const float* x, 
 // column sums of dy [M][d] (a bias gradient) as partial rows joining the pending batch
 int defer_colsum(const Ctx& C, const void* dy, float* part, long long goff, int accumulate) {
   int np = 0;
-  CK(cg_colsum_partials(C.dt, dy, C.D.d, (int)C.M, C.D.d, part, &np, C.s));
+  CK(cg_colsum_partials(C.dt, dy, C.D.d, (int)C.M, C.D.d, part, C.A.nb.ocp_half, &np, C.s));
   return defer_reduce(C.m, part, C.D.d, np, C.D.d, G(C, goff), accumulate, C.s);
 }
 
@@ -638,9 +652,11 @@ int aux_backward(const Ctx& C, int accumulate) {
       g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
       g.split_k = pick_split(C, ncp, d, M);
       g.workspace = A.splitws;
+    g.ws_bytes = A.nb.splitws;
+      g.ws_bytes = A.nb.splitws;
       CK(cg_gemm(&g, C.s));
       CK(cg_colsum(CG_F32, m->d_term_logits, m->ld_d_term, (int)M, nc, G(C, C.Lo.termb), accumulate, A.colws,
-                   C.s));
+                   A.nb.colws, C.s));
       // dxf += dT . W_t
       g = lin_dx(C, A.dlogits, ncp, C.Lo.termw, d, ncp, d, A.dtmp, d);
       g.c_dtype = CG_F32;
@@ -724,6 +740,7 @@ int aux_backward(const Ctx& C, int accumulate) {
     while (sk > 1 && (size_t)sk * D.Vp * d > A.splitws_floats) --sk;
     g.split_k = (int)sk;
     g.workspace = A.splitws;
+    g.ws_bytes = A.nb.splitws;
     CK(cg_gemm(&g, C.s));
     first += cnt;
   }
@@ -905,7 +922,7 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   CK(cg_cast_pad_2d(A.logits_pad, D.Vp, (int)M, D.V, CG_F32, m->logits, D.V, D.V, C.s));
   if (targets) {
     CK(cg_cross_entropy(A.logits_pad, D.Vp, targets, (int)M, D.V, m->cfg.label_smoothing, m->loss_weights, 0, 1.0f,
-                        C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, loss, A.cews, C.s));
+                        C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, loss, A.cews, A.nb.cews, C.s));
   }
   return CG_OK;
 }
@@ -981,6 +998,8 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       g.alpha = m->head_grad_scale;
       g.split_k = pick_split(C, D.Vp, d, M);
       g.workspace = A.splitws;
+    g.ws_bytes = A.nb.splitws;
+      g.ws_bytes = A.nb.splitws;
       CK(cg_gemm(&g, C.s));
       // dxf = s dlogits . E
       g = head_dx(C, hoff, A.dtmp, d);
@@ -1001,7 +1020,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     m->dw_done_layer = D.L;
     CK(cg_layernorm_bwd(CG_F32, A.dtmp, d, xL, d, A.meanf, A.rstdf, P(C, C.Lo.lnfw), nullptr, A.g, C.dt,
                         D.L > 0 ? A.slot[slot_of(D, ll)].gin : nullptr, site_seed(seed, ll, SITE_MLP), D.L > 0 ? p : 0.f, A.lnpart,
-                        G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), db2, accumulate, (int)M, d, eps, C.s));
+                        A.nb.lnp, G(C, C.Lo.lnfw), G(C, C.Lo.lnfb), db2, accumulate, (int)M, d, eps, C.s));
     CK(flush_reduce(m, C.s));  // the aux heads' bias gradients (their bucket is complete here)
     return CG_OK;
   }
@@ -1020,6 +1039,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       cg_gemm_desc g = lin_dx(C, sl.gin, d, o.w2, D.hid, d, D.hid, sl.dmlp, D.hid, a.w2T);
       g.epilogue = CG_EPI_DGELU | CG_EPI_GELU_DERIV | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
       g.workspace = sl.cpart;
+      g.ws_bytes = A.nb.cpart;
       CK(cg_gemm(&g, C.s));
       CK(defer_reduce(m, sl.cpart, D.hid, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
       g = lin_dx(C, sl.dmlp, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
@@ -1052,12 +1072,12 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (!D.rope)
       rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
                        C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, sl.bpart, D.Nqkv,
-                       A.delta, C.s);
+                       A.delta, A.nb.delta, C.s);
     const bool fused_bias = rc == CG_OK;
     if (rc == CG_EUNSUPPORTED)
       rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
                        C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, nullptr, 0,
-                       A.delta, C.s);
+                       A.delta, A.nb.delta, C.s);
     CK(rc);
     if (D.rope)
       CK(cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
@@ -1088,10 +1108,10 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
     const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
     CK(cg_embed_bwd(m->idx, A.g, G(C, C.Lo.tok), nullptr, C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
-                    acc_tok, A.embws, C.s));
+                    acc_tok, A.embws, A.nb.embws, C.s));
     if (C.Lo.pos >= 0)
       CK(cg_embed_bwd(m->idx, A.g, nullptr, G(C, C.Lo.pos), C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
-                      accumulate, A.embws, C.s));
+                      accumulate, A.embws, A.nb.embws, C.s));
     return CG_OK;
   }
   return CG_EINVAL;

@@ -641,6 +641,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   if ((p.epi & CG_EPI_DGELU) && !p.aux) return CG_EINVAL;
   if ((p.epi & CG_EPI_GELU_DERIV) && !(p.epi & (CG_EPI_GELU | CG_EPI_DGELU))) return CG_EINVAL;
   if ((p.epi & CG_EPI_COLSUM) && (!d->workspace || d->split_k > 1)) return CG_EINVAL;
+  if ((p.epi & CG_EPI_COLSUM) && d->ws_bytes < (size_t)cg_cdiv(p.M, 64) * (size_t)p.N * sizeof(float)) return CG_EINVAL;
   // SwiGLU epilogues: only the persistent bf16 tile implements them (the caller keeps the
   // separate cg_swiglu_* passes on CG_EUNSUPPORTED)
   const bool swg = (p.epi & (CG_EPI_SWIGLU | CG_EPI_DSWIGLU)) != 0;
@@ -658,7 +659,8 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
   if (d->K == 0) split = 1;
   int kchunk = cg_cdiv(cg_cdiv(d->K > 0 ? d->K : 1, split), bkt) * bkt;
   split = cg_cdiv(d->K > 0 ? d->K : 1, kchunk);
-  if (split > 1 && !d->workspace) return CG_EINVAL;
+  if (split > 1 && (!d->workspace || d->ws_bytes < (size_t)split * (size_t)p.M * (size_t)p.N * sizeof(float)))
+    return CG_EINVAL;
   p.kchunk = kchunk; p.split = split; p.ws = d->workspace;
   bool vec = false;
   const bool colsum = (p.epi & CG_EPI_COLSUM) != 0;
@@ -702,11 +704,29 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
                        : (d->b_kcontig ? gemm_bf16_kernel<false, true> : gemm_bf16_kernel<false, false>);
     }
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
-    const int pk = d->a_kcontig ? (d->b_kcontig ? CG_PROBE_GEMM_FWD : CG_PROBE_GEMM_DX)
-                                : (d->b_kcontig ? CG_PROBE_NONE : CG_PROBE_GEMM_DW);
+    // the persistent tile is one probe class (every forward and dX product of the step, all its
+    // epilogue specialisations); the other tiles are classed by operand layout
+    const int pk = pers ? CG_PROBE_GEMM_PERS
+                        : d->a_kcontig ? (d->b_kcontig ? CG_PROBE_GEMM_FWD : CG_PROBE_GEMM_DX)
+                                       : (d->b_kcontig ? CG_PROBE_NONE : CG_PROBE_GEMM_DW);
     cg_probe_begin(pk, s);
     hipLaunchKernelGGL(k, g, blk, sh, s, p);
-    cg_probe_end(pk, s, 2.0 * (double)p.M * (double)p.N * (double)p.K);
+    if (cg_probe_kind() == pk) {
+      // algorithmic work of the launch: the SwiGLU forward multiplies against both the gate and
+      // the up rows (2N weight rows); bytes = operands once + outputs once (+ epilogue operands)
+      const double M = p.M, N = p.N, K = p.K, ce = p.c_dtype == CG_F32 ? 4.0 : 2.0;
+      const bool sw = (p.epi & CG_EPI_SWIGLU) != 0, dsw = (p.epi & CG_EPI_DSWIGLU) != 0;
+      const double nb = sw ? 2.0 * N : N;  // weight rows read
+      double bytes = 2.0 * (M * K + nb * K) + M * N * ce;
+      if (p.epi & CG_EPI_BIAS) bytes += 4.0 * N;
+      if (p.epi & CG_EPI_RESID) bytes += 4.0 * M * N;
+      if (p.epi & (CG_EPI_GELU | CG_EPI_DGELU)) bytes += M * N * ce;
+      if (p.epi & CG_EPI_ACCUM) bytes += 4.0 * M * N;
+      if (sw) bytes += 2.0 * M * 2.0 * N;                   // pre-activations g|u
+      if (dsw) bytes += 2.0 * M * 2.0 * N + M * N * ce;     // g|u read, d(g|u) is 2N wide
+      if (p.epi & CG_EPI_COLSUM) bytes += 4.0 * cg_cdiv(p.M, 64) * N;
+      cg_probe_end(pk, s, 2.0 * M * nb * K, bytes);
+    }
   } else {
     return CG_EUNSUPPORTED;
   }
@@ -766,16 +786,20 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   const int grid = std::min(ntiles, cu_count());
   (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G::SMEM);
-  double flops = 0;
-  for (int i = 0; i < P.nprod; ++i) flops += 2.0 * P.p[i].N_out * (double)P.p[i].K_out * P.K;
+  double flops = 0, bytes = 0;
+  for (int i = 0; i < P.nprod; ++i) {
+    const bfd::Prod& q = P.p[i];
+    flops += 2.0 * q.N_out * (double)q.K_out * P.K;
+    bytes += 2.0 * P.K * ((double)q.N_out + q.K_out) + (q.accum ? 8.0 : 4.0) * q.N_out * (double)q.K_out;
+  }
   cg_probe_begin(CG_PROBE_GEMM_DW_GROUPED, s);
   hipLaunchKernelGGL((gemm_dw_kernel<BM, NS, BNT>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
-  cg_probe_end(CG_PROBE_GEMM_DW_GROUPED, s, flops);
+  cg_probe_end(CG_PROBE_GEMM_DW_GROUPED, s, flops, bytes);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }
 extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
-  if (!grp || grp->n < 0 || grp->n > CG_DW_MAX || grp->K <= 0 || grp->K % bfd::BKT) return CG_EINVAL;
+  if (!grp || grp->n < 0 || grp->n > CG_DW_MAX || grp->K <= 0) return CG_EINVAL;
   bfd::Params P{};
   P.nprod = 0;
   P.K = grp->K;

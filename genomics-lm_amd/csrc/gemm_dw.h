@@ -16,7 +16,10 @@
 // its tiles with one LDS-DMA ring that runs across tile seams (stages are addressed by a
 // global step index; steps past the end DMA from an out-of-range offset, which the buffer
 // range check turns into zero fills, so every wave issues the same number of VMEM ops and
-// the counted vmcnt waits stay exact).
+// the counted vmcnt waits stay exact).  The token count K need not be a multiple of the 64-row
+// k-step: the rows m >= K of the last step lie past the buffer's range end ((K-1)*ld + cols
+// elements), so they load as zeros and add nothing -- the dynamic-length loader's B*T
+// (data_loading.py:380-393 pads each batch only to its own longest sequence) runs as is.
 //
 // The MFMA operands are swapped (D^T = X_frag x dY_frag), so each lane ends with 4
 // consecutive output columns of each 16x16 block: the epilogue is 16-byte stores straight
@@ -83,7 +86,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
   const int nblk = gridDim.x;
   const int lb = cg_xcd_remap(blockIdx.x, nblk);  // an XCD's workgroups take consecutive tiles
   const int my_tiles = lb < P.ntiles ? (P.ntiles - 1 - lb) / nblk + 1 : 0;
-  const int nt = P.K / BKT;
+  const int nt = (P.K + BKT - 1) / BKT;  // a ragged last step reads rows >= K out of range: zero fill
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * (BNT / 2);
   if (my_tiles == 0) return;
 

@@ -196,14 +196,19 @@ extern "C" int cg_layernorm_bwd_blocks(int rows) {
   int b = cg_cdiv(rows, 16);
   return b > 1024 ? 1024 : (b < 1 ? 1 : b);
 }
+extern "C" size_t cg_layernorm_bwd_workspace(int rows, int cols, int want_col) {
+  return (size_t)cg_layernorm_bwd_blocks(rows) * (size_t)(want_col ? 3 : 2) * (size_t)(cols > 0 ? cols : 0) * sizeof(float);
+}
 
 // Vectorised backward: cols = 64*W*NV (runs as in ln_fwd_vec); one wave per row, per-lane
 // dgamma/dbeta partials in registers, combined across the block's 4 waves in LDS (fixed order).
+// g_in may alias g_out (the engine accumulates the residual gradient in place): each row's g_in
+// values are read before that row's g_out is written, and no other row touches them.
 template <typename TD, typename TO, int W, int NV>
 __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, long long lddy, const float* __restrict__ x,
                                                   long long ldx, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                                  const float* __restrict__ g_in, float* __restrict__ g_out,
+                                                  const float* g_in, float* g_out,
                                                   TO* __restrict__ g_out_t, uint32_t seed, uint32_t thr, float dscale,
                                                   float* __restrict__ partials, int rows, int want_col) {
   constexpr int cols = 64 * W * NV;
@@ -366,8 +371,8 @@ template <typename TD, typename TO>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, long long lddy,
                                                      const float* __restrict__ x, long long ldx,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma, const float* __restrict__ g_in,
-                                                     float* __restrict__ g_out, TO* __restrict__ g_out_t,
+                                                     const float* __restrict__ gamma, const float* g_in,
+                                                     float* g_out, TO* __restrict__ g_out_t,
                                                      uint32_t seed, uint32_t thr, float dscale,
                                                      float* __restrict__ partials, int rows, int cols,
                                                      int want_col) {
@@ -502,13 +507,14 @@ static int ln_bwd_rows(int dy_dtype, const void* dy, long long lddy, const float
 extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
                                 const float* mean, const float* rstd, const float* gamma, const float* g_in,
                                 float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
-                                float* partials, float* dgamma, float* dbeta, float* dcolsum, int accumulate,
-                                int rows, int cols, float eps, void* stream) {
+                                float* partials, size_t partials_bytes, float* dgamma, float* dbeta,
+                                float* dcolsum, int accumulate, int rows, int cols, float eps, void* stream) {
   (void)eps;
   if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
   if (dcolsum && (!g_out_t || !dgamma || !dbeta)) return CG_EINVAL;
   const int want_col = dcolsum ? 1 : 0;
   if (rows <= 0) return CG_OK;
+  if (!partials || partials_bytes < cg_layernorm_bwd_workspace(rows, cols, want_col)) return CG_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = cg_layernorm_bwd_blocks(rows);
   bool fast = false;
@@ -530,10 +536,12 @@ extern "C" int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, co
 extern "C" int cg_layernorm_bwd_partials(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
                                          const float* mean, const float* rstd, const float* gamma, const float* g_in,
                                          float* g_out, int out_dtype, void* g_out_t, uint32_t drop_seed, float drop_p,
-                                         float* partials, int want_col, int rows, int cols, void* stream) {
+                                         float* partials, size_t partials_bytes, int want_col, int rows, int cols,
+                                         void* stream) {
   if (cols <= 0 || cols > 64 * LN_MAXV) return CG_EUNSUPPORTED;
   if (!partials || (want_col && !g_out_t)) return CG_EINVAL;
   if (rows <= 0) return CG_OK;
+  if (partials_bytes < cg_layernorm_bwd_workspace(rows, cols, want_col)) return CG_EINVAL;
   bool fast = false;
   return ln_bwd_rows(dy_dtype, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, out_dtype, g_out_t, drop_seed, drop_p,
                      partials, want_col ? 1 : 0, rows, cols, (hipStream_t)stream, &fast);
@@ -718,10 +726,12 @@ __global__ void embed_bwd_pos_kernel(const float* __restrict__ g, float* __restr
 }
 
 extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, float* dpos, int B, int T, int V,
-                            int d, uint32_t drop_seed, float drop_p, int accumulate, void* ws, void* stream) {
+                            int d, uint32_t drop_seed, float drop_p, int accumulate, void* ws, size_t ws_bytes,
+                            void* stream) {
   if (V > 256) return CG_EUNSUPPORTED;
   const int rows = B * T;
   if (rows == 0) return CG_OK;
+  if (dtok && (!ws || ws_bytes < cg_embed_bwd_workspace(B, T, V, d))) return CG_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
@@ -1152,10 +1162,11 @@ static inline bool colsum_vec_ok(const void* X, long long ldx, int cols) {
 }
 
 extern "C" int cg_colsum_partials(int dtype, const void* X, long long ldx, int rows, int cols, float* part,
-                                  int* nparts, void* stream) {
+                                  size_t part_bytes, int* nparts, void* stream) {
   if (!nparts || (cols > 0 && (!X || !part))) return CG_EINVAL;
   *nparts = 0;
   if (cols <= 0 || rows <= 0) return CG_OK;
+  if (part_bytes < cg_colsum_workspace(rows, cols)) return CG_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   if (colsum_vec_ok(X, ldx, cols)) {
     const int nrb = cg_cdiv(rows, COLSUM_RB);
@@ -1179,10 +1190,10 @@ extern "C" int cg_colsum_partials(int dtype, const void* X, long long ldx, int r
 }
 
 extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out, int accumulate,
-                         void* ws, void* stream) {
+                         void* ws, size_t ws_bytes, void* stream) {
   if (cols == 0) return CG_OK;
   int np = 0;
-  const int rc = cg_colsum_partials(dtype, X, ldx, rows > 0 ? rows : 0, cols, (float*)ws, &np, stream);
+  const int rc = cg_colsum_partials(dtype, X, ldx, rows > 0 ? rows : 0, cols, (float*)ws, ws_bytes, &np, stream);
   if (rc != CG_OK) return rc;
   if (np == 0) {  // no rows: the sum is 0
     if (!accumulate && hipMemsetAsync(out, 0, (size_t)cols * 4, (hipStream_t)stream) != hipSuccess) return CG_ELAUNCH;
@@ -1320,8 +1331,10 @@ extern "C" size_t cg_ce_workspace(int rows) { return (size_t)(1 + ce_blocks(rows
 
 extern "C" int cg_cross_entropy(const float* logits, long long ldl, const int64_t* targets, int rows, int V,
                                 float eps, const float* class_w, int ignore_index, float grad_scale, int d_dtype,
-                                void* dlogits, long long ldd, float* loss, void* ws, void* stream) {
+                                void* dlogits, long long ldd, float* loss, void* ws, size_t ws_bytes,
+                                void* stream) {
   if (V > 128 || V <= 0) return CG_EUNSUPPORTED;
+  if (!ws || ws_bytes < cg_ce_workspace(rows)) return CG_EINVAL;
   hipStream_t s = (hipStream_t)stream;
   const int nblk = ce_blocks(rows);
   hipLaunchKernelGGL(ce_denom_kernel, dim3(1), dim3(1024), 0, s, targets, rows, class_w, ignore_index, (float*)ws);

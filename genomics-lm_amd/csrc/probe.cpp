@@ -14,6 +14,7 @@ struct Probe {
   std::vector<hipEvent_t> pool;  // pairs: start, stop
   size_t used = 0;
   double work = 0.0;
+  double bytes = 0.0;   // algorithmic HBM bytes of the recorded launches (operands once + outputs once)
   long long launches = 0;
   long long seen = 0;   // launches of the selected kernel since enable
   int every = 1;        // record 1 of every `every` launches (sampling keeps the event cost low)
@@ -42,7 +43,7 @@ void cg_probe_begin(int kind, hipStream_t s) {
   (void)hipEventRecord(g_probe.pool[g_probe.used], s);
 }
 
-void cg_probe_end(int kind, hipStream_t s, double work) {
+void cg_probe_end(int kind, hipStream_t s, double work, double bytes) {
   if (g_probe.kind != kind) return;
   std::lock_guard<std::mutex> lk(g_probe.mu);
   if (!g_probe.open) return;
@@ -50,6 +51,7 @@ void cg_probe_end(int kind, hipStream_t s, double work) {
   (void)hipEventRecord(g_probe.pool[g_probe.used + 1], s);
   g_probe.used += 2;
   g_probe.work += work;
+  g_probe.bytes += bytes;
   g_probe.launches += 1;
 }
 
@@ -58,6 +60,7 @@ extern "C" int cg_probe_enable(int kind) {
   g_probe.kind = kind;
   g_probe.used = 0;
   g_probe.work = 0.0;
+  g_probe.bytes = 0.0;
   g_probe.launches = 0;
   g_probe.seen = 0;
   g_probe.open = false;
@@ -84,5 +87,11 @@ extern "C" int cg_probe_read(double* work, double* ms, long long* launches) {
   if (work) *work = g_probe.work;
   if (ms) *ms = tot;
   if (launches) *launches = g_probe.launches;
+  return CG_OK;
+}
+
+extern "C" int cg_probe_bytes(double* bytes) {
+  std::lock_guard<std::mutex> lk(g_probe.mu);
+  if (bytes) *bytes = g_probe.bytes;
   return CG_OK;
 }

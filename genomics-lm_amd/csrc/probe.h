@@ -4,4 +4,5 @@
 
 int cg_probe_kind();
 void cg_probe_begin(int kind, hipStream_t s);
-void cg_probe_end(int kind, hipStream_t s, double work);
+// work: algorithmic FLOPs of the launch; bytes: its algorithmic HBM bytes (operands once + outputs once)
+void cg_probe_end(int kind, hipStream_t s, double work, double bytes = 0.0);

@@ -53,7 +53,8 @@ enum {
  * Replaces nn.Linear / matmul call sites of model_tiny_gpt.py:85-93,132,143-148,50-57,327
  * and their autograd (dX = dY W, dW = dY^T X).  Inputs are `in_dtype`; C is c_dtype.
  * Contiguous extents must be multiples of 8 and leading dims multiples of 8 elements.
- * split_k > 1 needs `workspace` of split_k*M*N floats (dW GEMMs).
+ * split_k > 1 needs `workspace` of split_k*M*N floats (dW GEMMs); CG_EPI_COLSUM needs
+ * ceil(M/64)*N floats.  ws_bytes is the workspace's size: a short one is CG_EINVAL.
  */
 typedef struct {
   int in_dtype, c_dtype;
@@ -69,6 +70,7 @@ typedef struct {
   uint32_t drop_seed; float drop_p;
   int split_k; float* workspace;
   int n_valid; /* SWIGLU / DSWIGLU: columns < n_valid are live (0 = all N) */
+  size_t ws_bytes; /* bytes at `workspace` */
 } cg_gemm_desc;
 int cg_gemm(const cg_gemm_desc* d, void* stream);
 /* bf16 tile selection: -1 auto (default; env CG_GEMM_WIDE overrides at load), 0 = 128x128
@@ -85,7 +87,8 @@ int cg_gemm_set_pers(int mode);
  * (dW = dY^T X of the nn.Linear call sites, A = dY and B = X both token-major bf16, C fp32).
  * Each output tile is reduced over all K rows inside one workgroup (no split-K partials);
  * the tiles of all products form one persistent launch (tile_m = 128 or 256 rows of C per
- * tile, 0 = default; env CG_DW_BM).  K % 64 == 0; N_out, K_out, lda, ldb % 8 == 0; ldc % 4. */
+ * tile, 0 = default; env CG_DW_BM).  Any K >= 1 (a ragged last 64-row k-step is zero-filled);
+ * N_out, K_out, lda, ldb % 8 == 0; ldc % 4. */
 #define CG_DW_MAX 32
 typedef struct {
   const void* A; long long lda;
@@ -112,14 +115,17 @@ int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* 
  * per-block column partials for dgamma/dbeta go to `partials` [nblk][2*cols]
  * (nblk = cg_layernorm_bwd_blocks(rows)), reduced into dgamma/dbeta (accumulate flag).
  * dcolsum (optional, needs g_out_t): column sums of g_out_t before rounding = the bias
- * gradient of the Linear that produced the branch g_out_t feeds (partials then [nblk][3*cols]). */
+ * gradient of the Linear that produced the branch g_out_t feeds (partials then [nblk][3*cols]).
+ * partials_bytes: the partials buffer's size, at least cg_layernorm_bwd_workspace(rows, cols,
+ * want_col = dcolsum != NULL), else CG_EINVAL.  g_in may equal g_out (in-place accumulation). */
 int cg_layernorm_bwd_blocks(int rows);
+size_t cg_layernorm_bwd_workspace(int rows, int cols, int want_col);
 int cg_layernorm_bwd(int dy_dtype, const void* dy, long long lddy, const float* x, long long ldx,
                      const float* mean, const float* rstd, const float* gamma,
                      const float* g_in, float* g_out, int out_dtype, void* g_out_t,
-                     uint32_t drop_seed, float drop_p, float* partials, float* dgamma,
-                     float* dbeta, float* dcolsum, int accumulate, int rows, int cols, float eps,
-                     void* stream);
+                     uint32_t drop_seed, float drop_p, float* partials, size_t partials_bytes,
+                     float* dgamma, float* dbeta, float* dcolsum, int accumulate, int rows, int cols,
+                     float eps, void* stream);
 /* the same backward without the reduction: only the partial rows are written,
  * [nblk][(2 + want_col) * cols] = dgamma | dbeta | (consumer column sums); they are reduced
  * later, batched with other layers' partials, by cg_reduce_columns (the engine defers the
@@ -128,7 +134,7 @@ int cg_layernorm_bwd_partials(int dy_dtype, const void* dy, long long lddy, cons
                               long long ldx, const float* mean, const float* rstd,
                               const float* gamma, const float* g_in, float* g_out, int out_dtype,
                               void* g_out_t, uint32_t drop_seed, float drop_p, float* partials,
-                              int want_col, int rows, int cols, void* stream);
+                              size_t partials_bytes, int want_col, int rows, int cols, void* stream);
 
 /* batched column reductions of partial rows (parameter / bias gradients, the backward of the
  * sums autograd performs per nn.Parameter): per job, dst[c] (+)= sum_r part[r * ld + c],
@@ -151,12 +157,12 @@ int cg_reduce_columns(const cg_reduce_batch* batch, void* stream);
 /* token + position embedding (+dropout) -- model_tiny_gpt.py:305-312 */
 int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const float* pos_emb, float* x,
                  int B, int T, int d, uint32_t drop_seed, float drop_p, void* stream);
-/* scatter-add backward into tok_emb grad (V rows) and pos grad; workspace size from
- * cg_embed_bwd_workspace(B,T,V,d) */
+/* scatter-add backward into tok_emb grad (V rows) and pos grad; with dtok, ws of ws_bytes >=
+ * cg_embed_bwd_workspace(B,T,V,d) bytes (else CG_EINVAL) */
 size_t cg_embed_bwd_workspace(int B, int T, int V, int d);
 int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, float* dpos, int B, int T,
                  int V, int d, uint32_t drop_seed, float drop_p, int accumulate, void* ws,
-                 void* stream);
+                 size_t ws_bytes, void* stream);
 
 /* segment starts from SEP ids: segstart[b,t] = last p<=t with idx[b,p]==sep (else 0);
  * build_attention_mask's cumsum(idx==sep) equality, model_tiny_gpt.py:289-294 */
@@ -189,7 +195,8 @@ int cg_attn_drop_mask(int B, int T, int H, uint32_t drop_seed, float drop_p, voi
  * forward's qkv rows (post-RoPE) and lse.  Inspection path. */
 int cg_attn_probs(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const float* lse,
                   float* out, int B, int T, int H, int KV, int hd, int window, void* stream);
-/* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: cg_attn_bwd_workspace().
+/* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: ws_bytes >= cg_attn_bwd_workspace()
+ * bytes (else CG_EINVAL).
  * bias_part (optional, bf16 MFMA path only -- CG_EUNSUPPORTED otherwise): fp32 column sums of
  * dqkv (before bf16 rounding) per (batch, 128-row tile), rows b*ceil(T/128) + tile, leading dim
  * ld_part >= (H + 2 KV) hd; reduced by cg_colsum_reduce into the q/k/v bias gradients. */
@@ -198,18 +205,18 @@ int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
                 const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
                 void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
                 uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
-                long long ld_part, void* ws, void* stream);
+                long long ld_part, void* ws, size_t ws_bytes, void* stream);
 
 /* Label-smoothed, class-weighted, ignore_index cross-entropy fwd+bwd over logits rows
  * (F.cross_entropy at model_tiny_gpt.py:343-349).  logits fp32 [rows][ldl], V used
  * columns; writes loss (1 float, mean per the reference weighting), dlogits (d_dtype
  * CG_F32 / CG_BF16 / CG_BF16X2, pad columns [V, ldd) -- per half for CG_BF16X2 -- zeroed)
- * scaled by `grad_scale`.  ws: cg_ce_workspace(rows) */
+ * scaled by `grad_scale`.  ws: ws_bytes >= cg_ce_workspace(rows) bytes (else CG_EINVAL) */
 size_t cg_ce_workspace(int rows);
 int cg_cross_entropy(const float* logits, long long ldl, const int64_t* targets, int rows,
                      int V, float eps, const float* class_w, int ignore_index,
                      float grad_scale, int d_dtype, void* dlogits, long long ldd,
-                     float* loss, void* ws, void* stream);
+                     float* loss, void* ws, size_t ws_bytes, void* stream);
 
 /* SwiGLU: s = silu(gu[:, :H]) * gu[:, Hp:Hp+H] (model_tiny_gpt.py:57) and backward */
 int cg_swiglu_fwd(int dtype, const void* gu, long long ldgu, int Hp, void* s, long long lds,
@@ -217,14 +224,15 @@ int cg_swiglu_fwd(int dtype, const void* gu, long long ldgu, int Hp, void* s, lo
 int cg_swiglu_bwd(int dtype, const void* gu, long long ldgu, int Hp, const void* ds,
                   long long ldds, void* dgu, long long lddgu, int rows, int H, void* stream);
 
-/* column sums (bias gradients): out[n] (+)= sum_m X[m*ldx+n] */
+/* column sums (bias gradients): out[n] (+)= sum_m X[m*ldx+n]; ws of ws_bytes >=
+ * cg_colsum_workspace(rows, cols) bytes (else CG_EINVAL) */
 size_t cg_colsum_workspace(int rows, int cols);
 int cg_colsum(int dtype, const void* X, long long ldx, int rows, int cols, float* out,
-              int accumulate, void* ws, void* stream);
-/* the first stage alone: *nparts partial rows [*nparts][cols] fp32 into part (sized by
+              int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* the first stage alone: *nparts partial rows [*nparts][cols] fp32 into part (part_bytes >=
  * cg_colsum_workspace), for a reduction batched with others (cg_reduce_columns) */
 int cg_colsum_partials(int dtype, const void* X, long long ldx, int rows, int cols, float* part,
-                       int* nparts, void* stream);
+                       size_t part_bytes, int* nparts, void* stream);
 
 /* out[c] (+)= sum_i part[i*cols + c] over nparts partial rows (the second stage of the fused
  * bias-gradient column sums, e.g. CG_EPI_COLSUM GEMM partials) */
@@ -431,13 +439,17 @@ enum {
   CG_PROBE_ATTN_FWD = 4,     /* attn_fwd_mfma                                      */
   CG_PROBE_ATTN_DQ = 5,      /* attn_bwd_dq_mfma                                   */
   CG_PROBE_ATTN_DKDV = 6,    /* attn_bwd_dkdv_mfma                                 */
-  CG_PROBE_GEMM_DW_GROUPED = 7 /* grouped weight-gradient GEMM (gemm_dw_kernel)      */
+  CG_PROBE_GEMM_DW_GROUPED = 7, /* grouped weight-gradient GEMM (gemm_dw_kernel)     */
+  CG_PROBE_GEMM_PERS = 8       /* persistent fwd / dX GEMM (gemm_bf16_pers_kernel, all */
+                               /* epilogue specialisations: one kernel class)           */
 };
 int cg_probe_enable(int kind);
 /* record 1 of every `every` launches of the probed kernel (default 1 = all); the launch
  * count and work returned by cg_probe_read cover the recorded launches only */
 int cg_probe_sample(int every);
 int cg_probe_read(double* work, double* ms, long long* launches);
+/* algorithmic HBM bytes (operands once + outputs once) of the same recorded launches */
+int cg_probe_bytes(double* bytes);
 
 const char* cg_version(void);
 

@@ -365,15 +365,17 @@ def test_attention_mfma_full_geometry(B, T, H, KV, hd, p):
         assert e <= 2e-2, (name, e)
 
 
+@pytest.mark.parametrize("K", [2048, 1023, 37])
 @pytest.mark.parametrize("tile", [128, 129, 256, 512])
-def test_gemm_dw_grouped_tiles(tile):
+def test_gemm_dw_grouped_tiles(tile, K):
     """Grouped full-reduction dW (cg_gemm_dw_grouped) for every tile code, against fp32 products
     of the same bf16 operands: ragged N_out / K_out (partial tiles), strided operands, alpha and
-    accumulate, products of different shapes in one launch.  Bound: fp32 accumulation of exact
-    bf16 products over K = 2048 rows -> max error <= 1e-5 of the output scale."""
+    accumulate, products of different shapes in one launch, and token counts K that are not a
+    multiple of the 64-row k-step (the dynamic-length loader's B*T; the last step's rows >= K are
+    zero-filled by the buffer range check).  Bound: fp32 accumulation of exact bf16 products over
+    K rows -> max error <= 1e-5 of the output scale."""
     ops = _ops()
-    g = torch.Generator().manual_seed(tile)
-    K = 2048
+    g = torch.Generator().manual_seed(tile + K)
     shapes = [(200, 136), (512, 384), (72, 520), (1536, 512)]
     prods, refs = [], []
     for i, (n, k) in enumerate(shapes):

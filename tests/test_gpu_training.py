@@ -238,3 +238,50 @@ def test_transfer_from_cfg_remaps_vocabulary_and_runs(tmp_path, monkeypatch):
     assert json.loads((tmp_path / "runs/tgt-run/vocabulary.json").read_text())["transfer"]["checkpoint"] == str(src_ck)
     assert ck["cfg"]["device_contract"] == "mps" and ck["cfg"]["device"].startswith("cuda")
     assert "transfer_from" not in ck["cfg"]  # consumed like the reference's cfg.pop
+
+
+def test_bf16_training_on_dynamic_length_batches(tmp_path, monkeypatch):
+    """The dynamic-length loader (flat X + lengths, data_loading.py:380-393) pads each batch only
+    to its own longest sequence, so B*T is arbitrary; the bf16 engine (the trainer's default
+    compute dtype) trains on such batches -- the grouped weight-gradient launch reduces over any
+    token count (a zero-filled ragged last k-step), with dropout on and bucketed batches."""
+    from codonlm_amd.engine import Engine
+    from codonlm_amd.training.loop import run_training
+    monkeypatch.chdir(tmp_path)
+    rng = np.random.default_rng(7)
+    T = 128
+    lens = rng.integers(20, T + 1, size=40)
+    flat = rng.integers(4, 68, size=int(lens.sum())).astype(np.int32)
+    for name, sl in (("train", slice(0, 30)), ("val", slice(30, 40)), ("test", slice(30, 40))):
+        s = np.concatenate([[0], np.cumsum(lens)])
+        parts = [flat[s[i]:s[i + 1]] for i in range(len(lens))][sl]
+        np.savez(tmp_path / f"{name}.npz", X=np.concatenate(parts), lengths=lens[sl])
+    config = _config(tmp_path, vocab_size=68, block_size=T, n_layer=3, n_head=2, n_embd=128, batch_size=3,
+                     grad_accum_steps=2, epochs=2, dropout=0.1, label_smoothing=0.05, compute_dtype="bf16",
+                     lr=3e-3, warmup_steps=1, bucket_batching=True, n_buckets=3)
+    itos = tmp_path / "itos.txt"
+    itos.write_text("\n".join(f"token_{i}" for i in range(68)) + "\n")
+    config["itos_path"] = str(itos)
+    cp = tmp_path / "config.yaml"
+    cp.write_text(yaml.safe_dump(config))
+    shapes = []
+    orig = Engine.forward
+
+    def record(self, idx, targets, **kw):
+        shapes.append(tuple(idx.shape))
+        return orig(self, idx, targets, **kw)
+
+    monkeypatch.setattr(Engine, "forward", record)
+    paths = {k: tmp_path / f"{k}.npz" for k in ("train", "val", "test")}
+    run_training(dict(config), _args(cp, paths, run_id="dyn-bf16"))
+    ragged = [s for s in shapes if (s[0] * s[1]) % 64]
+    assert len(ragged) >= len(shapes) // 2, shapes
+    rows = list(csv.reader((tmp_path / "runs/dyn-bf16/scores/curves.csv").open()))
+    assert len(rows) == 3 and all(np.isfinite(float(v)) for v in rows[2][1:3])
+    metrics = json.loads((tmp_path / "runs/dyn-bf16/scores/metrics.json").read_text())
+    assert metrics["status"] == "completed"
+    ck = torch.load(tmp_path / "runs/dyn-bf16/checkpoints/last.pt", map_location="cpu", weights_only=True)
+    # every train target that is not PAD, both epochs (the reference's consumed_train_tokens)
+    assert ck["consumed_train_tokens"] == 2 * int((lens[:30] - 1).sum())
+    assert ck["step"] >= 10 and ck["epoch"] == 2
+    assert all(torch.isfinite(v).all() for k, v in ck["model"].items() if v.is_floating_point())

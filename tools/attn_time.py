@@ -59,7 +59,7 @@ def main():
                                    dy.data_ptr(), dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0),
                                    B, T, H, H, hd, 0, seed, p, mask.data_ptr(),
                                    bp.data_ptr() if bp is not None else None, bp.stride(0) if bp is not None else 0,
-                                   ws.data_ptr(), st) == 0
+                                   ws.data_ptr(), ws.numel() * 4, st) == 0
 
         def msk():
             assert lib.cg_attn_drop_mask(B, T, H, seed, p, mask.data_ptr(), st) == 0
