@@ -101,36 +101,12 @@ def next_token(model: TinyGPT, device: torch.device, ctx_ids: List[int]) -> torc
     return logits[0, -1]
 
 
-@torch.no_grad()
-def generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: int, temperature: float = 1.0,
-             topk: int = 0, eos_idx: int | None = None) -> List[int]:
-    """Sampling loop of :185-214 (torch.multinomial on the device RNG)."""
-    ids = list(ctx_ids)
-    max_T = getattr(model, "block_size", None)
-    for _ in range(max_new):
-        logits = next_token(model, device, ids)
-        if temperature != 1.0:
-            logits = logits / max(1e-6, float(temperature))
-        probs = torch.softmax(logits, dim=-1)
-        if topk and topk > 0:
-            vals, idxs = torch.topk(probs, k=min(topk, probs.numel()))
-            next_id = idxs[torch.multinomial(vals, 1).item()].item()
-        else:
-            next_id = torch.multinomial(probs, 1).item()
-        ids.append(next_id)
-        if max_T is not None and len(ids) > max_T:
-            ids = ids[-max_T:]
-        if eos_idx is not None and next_id == eos_idx:
-            break
-    return ids
-
-
-@torch.no_grad()
-def greedy_generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: int,
-                    eos_idx: int | None = None, kv_cache: bool = True) -> List[int]:
-    """Deterministic argmax continuation (the parity form of ``generate``).  With ``kv_cache``
-    the prompt is prefilled once and each new token costs one cached decode step while the
-    context fits block_size; past it the reference's sliding re-forward takes over."""
+def _decode_loop(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: int, pick,
+                 eos_idx: int | None, kv_cache: bool) -> List[int]:
+    """The autoregressive loop of query_model.py:185-214 with a KV cache: the prompt is prefilled
+    once and each new token is one cached decode step (cg_model_decode) while the context fits
+    block_size; once it does not, the reference's sliding-window re-forward takes over.
+    ``pick(logits[V]) -> id`` chooses the next token."""
     ids = list(ctx_ids)
     max_T = getattr(model, "block_size", None)
     cache = None
@@ -141,7 +117,7 @@ def greedy_generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], ma
     for _ in range(max_new):
         if cache is None:
             logits = next_token(model, device, ids)
-        next_id = int(torch.argmax(logits).item())
+        next_id = int(pick(logits))
         ids.append(next_id)
         if max_T is not None and len(ids) > max_T:
             ids = ids[-max_T:]
@@ -153,6 +129,30 @@ def greedy_generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], ma
             else:  # the context reached block_size: slide and recompute like the reference
                 cache = None
     return ids
+
+
+@torch.no_grad()
+def generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: int, temperature: float = 1.0,
+             topk: int = 0, eos_idx: int | None = None, kv_cache: bool = True) -> List[int]:
+    """Sampling loop of :185-214: temperature, optional top-k, torch.multinomial on the device
+    RNG -- the same draws in the same order as the reference; the logits come from the KV cache
+    (one decode step per token) instead of a full re-forward of the prefix."""
+    def pick(logits):
+        if temperature != 1.0:
+            logits = logits / max(1e-6, float(temperature))
+        probs = torch.softmax(logits, dim=-1)
+        if topk and topk > 0:
+            vals, idxs = torch.topk(probs, k=min(topk, probs.numel()))
+            return idxs[torch.multinomial(vals, 1).item()].item()
+        return torch.multinomial(probs, 1).item()
+    return _decode_loop(model, device, ctx_ids, max_new, pick, eos_idx, kv_cache)
+
+
+@torch.no_grad()
+def greedy_generate(model: TinyGPT, device: torch.device, ctx_ids: List[int], max_new: int,
+                    eos_idx: int | None = None, kv_cache: bool = True) -> List[int]:
+    """Deterministic argmax continuation (the parity form of ``generate``), KV-cached the same way."""
+    return _decode_loop(model, device, ctx_ids, max_new, lambda lg: torch.argmax(lg).item(), eos_idx, kv_cache)
 
 
 @torch.no_grad()

@@ -852,9 +852,58 @@ def run_training(cfg: dict, args) -> None:
         _finish(is_main, ckpt_dir, scores_dir, run_id, t_wall0, st, accumulation_health, model, history, "stopped")
         return
     except Exception as exc:
+        if _is_oom(exc):  # loop.py:1501-1549: save last.pt, halve batch_size in the YAML, re-raise
+            _oom_safeguard(exc, is_main, lambda: payload(st.cur_epoch or (st.start_epoch + 1)), save,
+                           getattr(args, "config", None), cfg.get("primary_training_contract") is not None)
+            raise
         write_failure_meta(exc)
         raise
     _finish(is_main, ckpt_dir, scores_dir, run_id, t_wall0, st, accumulation_health, model, history, "completed")
+
+
+def _is_oom(exc: Exception) -> bool:
+    """The reference's test on the message (loop.py:1501-1502): HIP/torch allocation failures."""
+    s = str(exc).lower()
+    return "out of memory" in s or "oom" in s or "allocate" in s or "allocation" in s
+
+
+def _oom_safeguard(exc, is_main, make_payload, save, config_path, primary) -> None:
+    """OOM safeguard of loop.py:1503-1549: checkpoint last.pt with checkpoint_reason "oom", then
+    (unless the config is an immutable primary contract) rewrite the YAML with batch_size halved
+    and grad_accum_steps doubled so the next launch fits; the caller re-raises."""
+    if not is_main:
+        return
+    print("\n" + "=" * 80)
+    print("[OOM SAFEGUARD] Out-Of-Memory error detected during training loop execution!")
+    print(f"Error detail: {exc}")
+    print("Attempting to save last.pt checkpoint and downscale batch size in the config..." if not primary
+          else "Attempting to save last.pt without modifying the immutable config...")
+    print("=" * 80 + "\n")
+    try:
+        p = make_payload()
+        p["checkpoint_reason"] = "oom"
+        save(p, "last.pt")
+        print("[OOM SAFEGUARD] Gracefully saved checkpoint to last.pt.")
+    except Exception as save_exc:
+        print(f"[OOM SAFEGUARD] Failed to save checkpoint: {save_exc}")
+    if primary:
+        print("[OOM SAFEGUARD] Immutable primary config was not modified; "
+              "a new versioned runtime contract is required to change batch size.")
+        return
+    if not config_path or not os.path.isfile(config_path):
+        return
+    try:
+        import yaml
+        with open(config_path) as f:
+            data = yaml.safe_load(f) or {}
+        old_bs, old_gas = data.get("batch_size", 4), data.get("grad_accum_steps", 32)
+        data["batch_size"], data["grad_accum_steps"] = max(1, old_bs // 2), old_gas * 2
+        with open(config_path, "w") as f:
+            yaml.safe_dump(data, f)
+        print(f"[OOM SAFEGUARD] Config file {config_path} batch_size downscaled: {old_bs} -> {data['batch_size']} "
+              f"(grad_accum_steps doubled: {old_gas} -> {data['grad_accum_steps']})")
+    except Exception as yml_exc:
+        print(f"[OOM SAFEGUARD] Failed to update config: {yml_exc}")
 
 
 def _finish(is_main, ckpt_dir, scores_dir, run_id, t_wall0, st, health, model, history, status):

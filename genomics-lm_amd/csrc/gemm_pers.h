@@ -113,6 +113,20 @@ __device__ __forceinline__ float dpp_sum16(float t) {
   t += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x140, 0xF, 0xF, false));
   return t;
 }
+// diagnostic builds (timing only, results invalid): CG_PERS_DIAG=1 issues no operand DMAs after
+// the prologue, CG_PERS_DIAG=2 issues no MFMAs (fragment reads kept live)
+#ifndef CG_PERS_DIAG
+#define CG_PERS_DIAG 0
+#endif
+#if CG_PERS_DIAG == 2
+__device__ __forceinline__ v4f pmfma_diag(v8bf b, v8bf a, v4f c) {
+  asm volatile("" ::"v"(b), "v"(a));
+  return c;
+}
+#define PMFMA(b, a, c, x, y, z) bfp::pmfma_diag(b, a, c)
+#else
+#define PMFMA(b, a, c, x, y, z) __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, x, y, z)
+#endif
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -264,19 +278,21 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
     for (int gr = 0; gr < 8; ++gr) {
       const int i = gr >> 1, j0 = 2 * (gr & 1);
-      acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0], af[0][i], acc[i][j0], 0, 0, 0);
-      acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
+      acc[i][j0] = PMFMA(bfr[0][j0], af[0][i], acc[i][j0], 0, 0, 0);
+      acc[i][j0 + 1] = PMFMA(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
       if (gr < 4) af[1][gr] = bfg::frag<true>(as, wm + 16 * gr, 1, lane);
       else bfr[1][gr - 4] = bfrag(bs, wn, gr - 4, 1, lane);
-      if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
-      else if (gr < A_CHUNKS + B_CHUNKS)
-        bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
+      if (CG_PERS_DIAG != 1) {
+        if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
+        else if (gr < A_CHUNKS + B_CHUNKS)
+          bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
+        acc[i][j] = PMFMA(bfr[1][j], af[1][i], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
     for (int gr = 0; gr < 8; ++gr) {
@@ -330,20 +346,22 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
     for (int gr = 0; gr < 8; ++gr) {
       const int i = gr >> 1, j0 = 2 * (gr & 1);
-      acc[i][j0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0b[j0], f0a[i], acc[i][j0], 0, 0, 0);
-      acc[i][j0 + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f0b[j0 + 1], f0a[i], acc[i][j0 + 1], 0, 0, 0);
+      acc[i][j0] = PMFMA(f0b[j0], f0a[i], acc[i][j0], 0, 0, 0);
+      acc[i][j0 + 1] = PMFMA(f0b[j0 + 1], f0a[i], acc[i][j0 + 1], 0, 0, 0);
       if (gr < 4) af1[gr] = bfg::frag<true>(as, wm + 16 * gr, 1, lane);
       else bf1[gr - 4] = bfrag(bs, wn, gr - 4, 1, lane);
-      if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
-      else if (gr < A_CHUNKS + B_CHUNKS)
-        bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
+      if (CG_PERS_DIAG != 1) {
+        if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
+        else if (gr < A_CHUNKS + B_CHUNKS)
+          bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
+      }
     }
     if constexpr (MID) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = PMFMA(bf1[j], af1[i], acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int gr = 0; gr < 8; ++gr) {
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
@@ -361,7 +379,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       for (int i = 2; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = PMFMA(bf1[j], af1[i], acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int gr = 0; gr < 8; ++gr) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -372,7 +390,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf1[j], af1[i], acc[i][j], 0, 0, 0);
+          acc[i][j] = PMFMA(bf1[j], af1[i], acc[i][j], 0, 0, 0);
 #pragma unroll
       for (int gr = 0; gr < 8; ++gr) {
         __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);

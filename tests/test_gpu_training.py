@@ -285,3 +285,34 @@ def test_bf16_training_on_dynamic_length_batches(tmp_path, monkeypatch):
     assert ck["consumed_train_tokens"] == 2 * int((lens[:30] - 1).sum())
     assert ck["step"] >= 10 and ck["epoch"] == 2
     assert all(torch.isfinite(v).all() for k, v in ck["model"].items() if v.is_floating_point())
+
+
+def test_oom_safeguard_checkpoints_and_downscales_config(tmp_path, monkeypatch):
+    """loop.py:1501-1549: an allocation failure inside the loop saves last.pt with
+    checkpoint_reason "oom", halves batch_size / doubles grad_accum_steps in the YAML, re-raises."""
+    from codonlm_amd.engine import Engine
+    from codonlm_amd.training.loop import run_training
+    monkeypatch.chdir(tmp_path)
+    rng = np.random.default_rng(4)
+    seq = rng.integers(4, 68, size=(16, 33)).astype(np.int32)
+    config = _config(tmp_path, vocab_size=68, block_size=32, batch_size=4, grad_accum_steps=2, epochs=1,
+                     compute_dtype="bf16")
+    config_path, paths = _write_inputs(tmp_path, config, seq[:12, :-1], seq[:12, 1:], seq[12:, :-1], seq[12:, 1:],
+                                       V=68)
+    orig = Engine._ensure_workspace
+    calls = {"n": 0}
+
+    def failing(self, B, T):
+        calls["n"] += 1
+        if calls["n"] == 3:
+            raise torch.cuda.OutOfMemoryError("HIP out of memory. Tried to allocate 288.00 GiB")
+        return orig(self, B, T)
+
+    monkeypatch.setattr(Engine, "_ensure_workspace", failing)
+    with pytest.raises(torch.cuda.OutOfMemoryError):
+        run_training(dict(config), _args(config_path, paths, run_id="oom-run"))
+    ck = torch.load(tmp_path / "runs/oom-run/checkpoints/last.pt", map_location="cpu", weights_only=True)
+    assert ck["checkpoint_reason"] == "oom"
+    assert ck["step"] == 1  # the first group of 2 committed before the failing 3rd microbatch
+    new = yaml.safe_load(config_path.read_text())
+    assert new["batch_size"] == 2 and new["grad_accum_steps"] == 4

@@ -26,6 +26,20 @@ def timer(fn, it=10):
     return s.elapsed_time(e) / it * 1e3  # us
 
 
+def probe_bytes(fn):
+    """algorithmic (FLOPs, HBM bytes) of one call, from the library's probe (persistent class)"""
+    import ctypes as C
+    L.lib.cg_probe_sample(1)
+    L.lib.cg_probe_enable(L.PROBE_GEMM_PERS)
+    fn()
+    torch.cuda.synchronize()
+    w, ms, k, b = C.c_double(0), C.c_double(0), C.c_longlong(0), C.c_double(0)
+    L.lib.cg_probe_read(C.byref(w), C.byref(ms), C.byref(k))
+    L.lib.cg_probe_bytes(C.byref(b))
+    L.lib.cg_probe_enable(0)
+    return w.value, b.value
+
+
 def main():
     g = torch.Generator().manual_seed(0)
     bf = lambda *s: torch.randn(*s, generator=g).to(dev, torch.bfloat16)  # noqa: E731
@@ -95,11 +109,15 @@ def main():
     for name, N, K, f, f0 in rows:
         fl = 2.0 * M * N * K
         te = best[(name, "epi")]
+        pw, pb = probe_bytes(f)
+        # roofline time of the product: max(FLOPs at 2.5 PF, algorithmic bytes at 8 TB/s)
+        bound = max(pw / 2.5e15, pb / 8e12) * 1e6 if pw else 0.0
         if not name.endswith(" only") and name != "colsum reduce":  # the step's own products
             tot += te
         tp = best.get((name, "plain"))
         extra = f"  plain {tp:6.1f} us {fl / tp / 1e6:6.1f} TF/s" if tp else ""
-        print(f"{name:32s} N={N:5d} K={K:5d} {te:6.1f} us {fl / te / 1e6:6.1f} TF/s{extra}", flush=True)
+        print(f"{name:32s} N={N:5d} K={K:5d} {te:6.1f} us {fl / te / 1e6:6.1f} TF/s  {pb / 1e6:6.1f} MB "
+              f"{pb / te / 1e6:5.2f} TB/s  roof {bound:5.1f} us ({bound / te:4.2f}){extra}", flush=True)
     if only is None:
         print(f"sum per layer {tot:.1f} us  (x12 = {tot * 12 / 1e3:.2f} ms)")
 
