@@ -461,6 +461,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
 
 #include "gemm_wide.h"
 #include "gemm_pers.h"
+#include "gemm_lw.h"
 #include "gemm_dw.h"
 
 // CG_EPI_COLSUM fallback: part[r/64][n] = sum of C rows [64r, 64r+64) (column n)
@@ -518,9 +519,24 @@ template <bool AK, bool BKC, int E, int T>
 struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC, E, T>; };
 
 // persistent 256x128 tile (K-contiguous operands only, compile-time epilogues only)
+// loader-wave variant (gemm_lw.h) for the products without an epilogue or with a bias only:
+// measured per C4 product (tools/gemm_c4.py, CG_PERS_LW=0/1 interleaved on one box) it takes
+// qkv dX 28.3 -> 26.9 us, fc1 dX 35.0 -> 32.7, qkv fwd and proj dX unchanged, while the
+// VALU- and memory-heavy epilogues (GELU, dGELU + column sums, fp32 residual) ran 1.2-2.3 us
+// slower in it -- those keep gemm_bf16_pers_kernel.  CG_PERS_LW=0 (env, read at load): never,
+// 2: for every epilogue it implements.
+static int g_pers_lw = [] {
+  const char* e = getenv("CG_PERS_LW");
+  return e ? atoi(e) : 1;
+}();
+// the SwiGLU backward's epilogue does not fit the loader-wave kernel's 168-register budget
+static bool pers_lw_for(int e) {
+  if (g_pers_lw == 2) return e != CG_EPI_DSWIGLU;
+  return g_pers_lw == 1 && (e == 0 || e == CG_EPI_BIAS);
+}
 static gemm_kernel_t pick_pers(int e, int ct) {
 #define PSPEC(E, T) \
-  if (e == (E) && ct == (T)) return gemm_bf16_pers_kernel<(E), (T)>;
+  if (e == (E) && ct == (T)) return pers_lw_for(e) ? gemm_bf16_lw_kernel<(E), (T)> : gemm_bf16_pers_kernel<(E), (T)>;
   PSPEC(0, CG_BF16)
   PSPEC(0, CG_F32)
   PSPEC(CG_EPI_BIAS, CG_BF16)
@@ -690,7 +706,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
       colsum_fused = colsum;
       const int tiles = cg_cdiv(p.N, (p.epi & CG_EPI_SWIGLU) ? bfp::BN / 2 : bfp::BN) * cg_cdiv(p.M, bfp::BM);
       g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cu_count()));
-      blk = dim3(bfp::THREADS);
+      blk = dim3(pers_lw_for(p.epi) ? bfl::THREADS : bfp::THREADS);
       sh = bfp::SMEM;
     } else if (vec && use_wide(d, kchunk, split)) {
       k = pick_spec<WideK>(d->a_kcontig, d->b_kcontig, ke, kt);

@@ -118,6 +118,9 @@ __device__ __forceinline__ float dpp_sum16(float t) {
 #ifndef CG_PERS_DIAG
 #define CG_PERS_DIAG 0
 #endif
+#ifndef CG_PERS_L2HOT
+#define CG_PERS_L2HOT 0
+#endif
 #if CG_PERS_DIAG == 2
 __device__ __forceinline__ v4f pmfma_diag(v8bf b, v8bf a, v4f c) {
   asm volatile("" ::"v"(b), "v"(a));
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       ao = bo = OOR;
       return;
     }
-    const int k = g / nt, t = g - k * nt;
+    const int k = g / nt, t = (CG_PERS_DIAG == 5 || CG_PERS_L2HOT) ? 0 : g - k * nt;  // diag 5: every step re-reads k-step 0 (L2-hot)
     int m0, n0;
     tile_org(k, m0, n0);
     ao = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
@@ -690,6 +693,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       epilogue(k);
     }
   };
+  // diagnostic 3 (timing only: LDS hazards): waves 4-7 one barrier behind waves 0-3 (a stagger);
+  // 4: waves 4-7 at issue priority 1 for the whole kernel
+  if (CG_PERS_DIAG == 3 && wave >= 4) __builtin_amdgcn_s_barrier();
+  if (CG_PERS_DIAG == 4 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 #ifndef CG_PERS_NO_SPREAD
   const int np = NL == 0 ? 0 : nt >= 7 ? 4 : nt >= 5 ? 2 : nt >= 4 ? 1 : 0;
 #else
@@ -703,5 +710,6 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     else if (np == 1) tiles(std::integral_constant<int, 1>{});
     else tiles(std::integral_constant<int, 0>{});
   }
+  if (CG_PERS_DIAG == 3 && wave < 4) __builtin_amdgcn_s_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
 }
