@@ -120,6 +120,10 @@ SIGNATURES = {
     "cg_gemm": (i32, [C.POINTER(GemmDesc), vp]),
     "cg_gemm_set_wide": (i32, [i32]),
     "cg_gemm_set_pers": (i32, [i32]),
+    "cg_set_cu_reserve": (i32, [i32]),
+    "cg_gemm_set_pers_lw": (i32, [i32]),
+    "cg_pers_cus": (i32, []),
+    "cg_diag_occupy": (i32, [i32, i32, vp]),
     "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),
     "cg_gemm_dw_tiles": (i32, [i32, i32, i32]),
     "cg_gemm_dw_set_tile": (i32, [i32]),

@@ -49,16 +49,6 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   return true;
 }
 
-int device_cus() {
-  static int n = 0;
-  if (!n) {
-    int dev = 0, v = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
-    n = v;
-  }
-  return n;
-}
 // Group size and tiles of the grouped dW launches (bf16 engine).  A group's tiles run as one
 // persistent launch with one workgroup per CU and every tile costing about the same (full-token
 // reduction), so a group takes ceil(tiles / CUs) rounds of its tile's cost.  Tile candidates
@@ -77,7 +67,7 @@ static int dw_forced_bm() {
 }
 // cheapest tile for a group of n blocks, and its cost
 static int dw_tile_for(const Dims& D, int n, double* cost_out) {
-  const int d = D.d, cus = device_cus();
+  const int d = D.d, cus = cg_pers_cus();
   int best = 256;
   double best_cost = 1e30;
   for (int bm : {128, 256, 512}) {
@@ -526,9 +516,20 @@ int bias_grad(const Ctx& C, const void* dy, long long lddy, int N, long long gof
 
 float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 
-// position of block l inside its dW group (groups run from block L-1 downwards)
-int slot_of(const Dims& D, int l) { return (D.L - 1 - l) % D.G; }
-bool group_ends(const Dims& D, int l) { return l == 0 || slot_of(D, l) == D.G - 1; }
+// dW groups run from block L-1 downwards; the short remainder group (L mod G blocks) comes FIRST,
+// so the first blocks' gradient buckets are final -- and their data-parallel all-reduce starts --
+// after that group instead of after G blocks (C4: groups of 2, 5, 5 from the top)
+int first_group(const Dims& D) { return D.L % D.G ? D.L % D.G : D.G; }
+// position of block l inside its group, counted from the group's top block
+int slot_of(const Dims& D, int l) {
+  const int u = D.L - 1 - l, f = first_group(D);
+  return u < f ? u : (u - f) % D.G;
+}
+bool group_ends(const Dims& D, int l) {
+  if (l == 0) return true;
+  const int u = D.L - 1 - l, f = first_group(D);
+  return u < f ? u == f - 1 : slot_of(D, l) == D.G - 1;
+}
 
 // Parameter / bias gradient reductions deferred to the end of a dW group: the LayerNorm
 // backward and the fused column-sum epilogues of a group's blocks leave partial rows in their

@@ -519,16 +519,22 @@ template <bool AK, bool BKC, int E, int T>
 struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC, E, T>; };
 
 // persistent 256x128 tile (K-contiguous operands only, compile-time epilogues only)
-// loader-wave variant (gemm_lw.h) for the products without an epilogue or with a bias only:
-// measured per C4 product (tools/gemm_c4.py, CG_PERS_LW=0/1 interleaved on one box) it takes
-// qkv dX 28.3 -> 26.9 us, fc1 dX 35.0 -> 32.7, qkv fwd and proj dX unchanged, while the
-// VALU- and memory-heavy epilogues (GELU, dGELU + column sums, fp32 residual) ran 1.2-2.3 us
-// slower in it -- those keep gemm_bf16_pers_kernel.  CG_PERS_LW=0 (env, read at load): never,
-// 2: for every epilogue it implements.
+// loader-wave variant (gemm_lw.h).  Measured per C4 product (tools/gemm_c4.py, CG_PERS_LW=0/1
+// interleaved on one box) it takes qkv dX 28.3 -> 26.9 us and fc1 dX 35.0 -> 32.7 us (qkv fwd
+// and proj dX unchanged), while the VALU- and memory-heavy epilogues (GELU, dGELU + column sums,
+// fp32 residual) run 1.2-2.3 us slower in it; with it on the plain / bias-only products the
+// whole C4 step measured 8.45 vs 8.41 ms (bench.py, 2 x 2 interleaved runs on one box) -- so it
+// is off by default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
+// products without an epilogue or with a bias only, 2 for every epilogue it implements.
 static int g_pers_lw = [] {
   const char* e = getenv("CG_PERS_LW");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }();
+extern "C" int cg_gemm_set_pers_lw(int mode) {
+  const int old = g_pers_lw;
+  g_pers_lw = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
+  return old;
+}
 // the SwiGLU backward's epilogue does not fit the loader-wave kernel's 168-register budget
 static bool pers_lw_for(int e) {
   if (g_pers_lw == 2) return e != CG_EPI_DSWIGLU;
@@ -578,6 +584,19 @@ static int cu_count() {
   }
   return n[dev];
 }
+// CUs the persistent launches (forward / dX tiles, grouped dW) spread over: all of them, minus a
+// reserve left free for kernels that run beside them (the RCCL all-reduce of a data-parallel
+// backward, which otherwise holds CUs a one-tile-per-CU launch is waiting for)
+static int g_cu_reserve = [] {
+  const char* e = getenv("CG_PERS_CU_RESERVE");
+  return e ? std::max(0, atoi(e)) : 0;
+}();
+extern "C" int cg_set_cu_reserve(int n) {
+  const int old = g_cu_reserve;
+  g_cu_reserve = n < 0 ? 0 : n;
+  return old;
+}
+extern "C" int cg_pers_cus(void) { return std::max(1, cu_count() - g_cu_reserve); }
 static bool use_pers(const cg_gemm_desc* d, int split) {
   if (!g_pers_mode || split != 1) return false;
   if (!d->a_kcontig || !d->b_kcontig) return false;
@@ -705,7 +724,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
       k = pick_pers(p.epi, p.c_dtype);
       colsum_fused = colsum;
       const int tiles = cg_cdiv(p.N, (p.epi & CG_EPI_SWIGLU) ? bfp::BN / 2 : bfp::BN) * cg_cdiv(p.M, bfp::BM);
-      g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cu_count()));
+      g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cg_pers_cus()));
       blk = dim3(pers_lw_for(p.epi) ? bfl::THREADS : bfp::THREADS);
       sh = bfp::SMEM;
     } else if (vec && use_wide(d, kchunk, split)) {
@@ -799,7 +818,7 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   }
   P.ntiles = ntiles;
   if (!ntiles) return CG_OK;
-  const int grid = std::min(ntiles, cu_count());
+  const int grid = std::min(ntiles, cg_pers_cus());
   (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G::SMEM);
   double flops = 0, bytes = 0;

@@ -1829,3 +1829,28 @@ extern "C" int cg_transpose16_batch(const cg_transpose_batch* tb, void* stream) 
   CG_LAUNCH_CHECK();
   return CG_OK;
 }
+
+// ===========================================================================
+// diagnostic CU occupier (cg_diag_occupy): each workgroup takes a whole CU (all of its LDS) and
+// sleeps until the deadline on the 100 MHz real-time counter; every wave reaches the exit.
+// ===========================================================================
+__global__ __launch_bounds__(1024) void diag_occupy_kernel(long long ticks) {
+  extern __shared__ char hold[];
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) hold[0] = 0;
+  while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
+extern "C" int cg_diag_occupy(int n_cus, int usec, void* stream) {
+  if (n_cus <= 0 || usec <= 0) return CG_OK;
+  if (usec > 10 * 1000 * 1000) return CG_EINVAL;  // bounded: at most 10 s
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)diag_occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(diag_occupy_kernel, dim3(n_cus), dim3(1024), 160 * 1024, (hipStream_t)stream,
+                     (long long)usec * 100);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}

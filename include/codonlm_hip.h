@@ -81,6 +81,15 @@ int cg_gemm_set_wide(int mode);
  * N > 1 = whenever legal with the grid capped at N workgroups (each walks more tiles).
  * Returns the previous mode. */
 int cg_gemm_set_pers(int mode);
+/* CUs left free by the persistent launches (forward / dX tiles, grouped dW): they spread over
+ * (CU count - reserve) workgroups; env CG_PERS_CU_RESERVE sets it at load.  Returns the previous
+ * reserve.  cg_pers_cus: the CU count those launches (and the dW planner) use now. */
+int cg_set_cu_reserve(int n);
+/* persistent-tile variant with dedicated LDS-DMA loader waves (gemm_lw.h): 0 off (default; env
+ * CG_PERS_LW at load), 1 for products without an epilogue or with a bias only, 2 wherever it
+ * implements the epilogue.  Returns the previous mode. */
+int cg_gemm_set_pers_lw(int mode);
+int cg_pers_cus(void);
 
 /* Grouped weight-gradient GEMM: for every product p of the group
  *   C_p[n][k] (+)= alpha_p * sum_{m < K} A_p[m*lda_p + n] * B_p[m*ldb_p + k]
@@ -450,6 +459,11 @@ int cg_probe_sample(int every);
 int cg_probe_read(double* work, double* ms, long long* launches);
 /* algorithmic HBM bytes (operands once + outputs once) of the same recorded launches */
 int cg_probe_bytes(double* bytes);
+
+/* diagnostic: occupy n_cus CUs (one 1024-thread workgroup holding all 160 KiB of LDS each) for
+ * `usec` microseconds on `stream` -- stands in for kernels that run beside the step (an RCCL
+ * all-reduce) when measuring the persistent launches' sensitivity to busy CUs */
+int cg_diag_occupy(int n_cus, int usec, void* stream);
 
 const char* cg_version(void);
 

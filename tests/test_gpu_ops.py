@@ -553,16 +553,18 @@ def test_transpose16_batch():
         assert torch.equal(o.cpu(), m.cpu().t())
 
 
+@pytest.mark.parametrize("lw", [0, 2])
 @pytest.mark.parametrize("cap", [1, 3])
 @pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256), (600, 200, 320),
                                    (520, 264, 512)])
-def test_gemm_persistent_tile_epilogues(cap, M, N, K):
+def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     """Persistent 256x128 tile (K-contiguous operands): every compile-time epilogue, partial
     M/N tiles, and (cap=3) a grid of 3 workgroups that each walk many tiles, so the LDS-DMA ring
     and the counted waits carry across tile boundaries with epilogue stores in flight.  K = 128 /
     192 issue the epilogue loads in the last k-step; K = 256 / 320 / 512 spread them over the
     tile's last 1 / 2 / 4 k-steps.  CG_EPI_GELU_DERIV: the forward stores gelu'(pre) and the
-    backward multiplies by it."""
+    backward multiplies by it.  lw=2: the same on the loader-wave variant (gemm_lw.h) for every
+    epilogue it implements."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
     g = torch.Generator().manual_seed(M + N + K)
@@ -574,6 +576,7 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K):
     base = _bf(x) @ _bf(w).t()
     tol = 3e-2 * 4
     old = L.lib.cg_gemm_set_pers(cap)
+    old_lw = L.lib.cg_gemm_set_pers_lw(lw)
     try:
         y0 = ops.gemm(xd, wd, out_dtype=torch.float32)
         y0b = ops.gemm(xd, wd, out_dtype=torch.bfloat16)
@@ -602,6 +605,7 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K):
         torch.cuda.synchronize()
     finally:
         L.lib.cg_gemm_set_pers(old)
+        L.lib.cg_gemm_set_pers_lw(old_lw)
     pre = base + bias
     assert (y0.cpu() - base).abs().max() < tol
     assert (y0b.float().cpu() - base).abs().max() < tol + 0.01 * base.abs().max()

@@ -1,12 +1,16 @@
-"""HBM traffic per launch of the grouped dW kernel from the two rocprofv3 PMC passes that
-tools/prof_round2.sh collects (FETCH_SIZE and WRITE_SIZE in separate runs), against the
-kernel's algorithmic bytes; writes profiles/round2/pmc_traffic_<cfg>.json (read by bench.py).
+"""HBM traffic per launch of a probed kernel class from the two rocprofv3 PMC passes that
+tools/prof_round3.sh collects (FETCH_SIZE and WRITE_SIZE in separate runs), against the class's
+algorithmic bytes per launch; writes profiles/<round>/pmc_traffic_<cfg>_<probe>.json (bench.py
+attaches it to its roofline line as `traffic`).
 
-    python tools/pmc_traffic.py gpurun_out/r2_c4 c4 <commit>
+    python tools/pmc_traffic.py gpurun_out/r3_c4 c4 <commit> gemm_bf16_pers gpurun_out/r3_c4/bench.json [round3]
 
-HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB units; gfx950 counts wide streaming reads at
-half, MI355X_MICROARCH.md HBM/rocprofv3 section).  Algorithmic bytes of a launch = the dY and X
-operands (bf16) once + dW (fp32) once for every block of its group."""
+HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB units; gfx950 counts wide streaming reads at half,
+MI355X_MICROARCH.md HBM/rocprofv3 section), averaged over every launch of the class in the passes.
+Algorithmic bytes per launch = the bench line's `roofline.algorithmic_bytes_per_launch` (the
+library's probe: operands once + outputs once + epilogue operands, summed over the sampled launches
+of the timed region) -- or, for gemm_dw_grouped, the dY / X operands (bf16) once + dW (fp32) once per
+block of each launch's group."""
 import csv
 import glob
 import json
@@ -17,21 +21,25 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 from bench import CONFIGS  # noqa: E402
 
-KERNEL = "gemm_dw_kernel"
+PREFIX = {"gemm_bf16_pers": ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel"), "gemm_dw_grouped": ("gemm_dw_kernel",),
+          "attn_fwd_mfma": ("attn_fwd_mfma",), "attn_bwd_dq_mfma": ("attn_bwd_dq_mfma",),
+          "attn_bwd_dkdv_mfma": ("attn_bwd_dkdv_mfma",)}
 
 
-def launches(d, counter):
+def launches(d, counter, prefixes):
     rows = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
-                rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024))
+            name = r["Kernel_Name"]
+            if any(name.startswith("void " + p) or name.startswith(p) for p in prefixes) and \
+                    r["Counter_Name"] == counter:
+                rows.append((int(r["Dispatch_Id"]), name, float(r["Counter_Value"]) * 1024))
     rows.sort()
     return rows
 
 
-def block_bytes(c):
-    d, L = c["n_embd"], c["n_layer"]
+def dw_block_bytes(c):
+    d = c["n_embd"]
     hd = d // c["n_head"]
     kvd = (c["kv"] or c["n_head"]) * hd
     nqkv = d + 2 * kvd
@@ -45,29 +53,41 @@ def block_bytes(c):
 
 
 def main():
-    d, cfg, commit = sys.argv[1], sys.argv[2], sys.argv[3]
+    d, cfg, commit, probe = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
+    bench_json = sys.argv[5] if len(sys.argv) > 5 else None
+    rnd = sys.argv[6] if len(sys.argv) > 6 else "round3"
     c = CONFIGS[cfg]
-    fetch, write = launches(f"{d}/pmc_fetch", "FETCH_SIZE"), launches(f"{d}/pmc_write", "WRITE_SIZE")
+    pre = PREFIX[probe]
+    fetch, write = launches(f"{d}/pmc_fetch", "FETCH_SIZE", pre), launches(f"{d}/pmc_write", "WRITE_SIZE", pre)
     assert fetch and len(fetch) == len(write), (len(fetch), len(write))
-    per_block, dw_block = block_bytes(c)
     out = []
     for (_, name, fb), (_, _, wb) in zip(fetch, write):
-        # the launch writes its blocks' fp32 dW once: WRITE_SIZE / dW bytes per block = group size
-        blocks = max(1, round(wb / dw_block))
-        out.append({"kernel": name, "blocks": blocks, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": 2 * fb + wb,
-                    "algorithmic_bytes": blocks * per_block})
-    res = {"probe": "gemm_dw_grouped", "kernel": sorted({o["kernel"] for o in out}), "config": cfg, "commit": commit,
+        out.append({"kernel": name, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": 2 * fb + wb})
+    res = {"probe": probe, "kernel": sorted({o["kernel"] for o in out}), "config": cfg, "commit": commit,
+           "launches_counted": len(out),
            "hbm_bytes_per_launch": round(sum(o["hbm_bytes"] for o in out) / len(out)),
            "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of `python "
                      "bench.py --steps 3 --warmup 2 --no-cpu-baseline --no-kernel-roofline`; HBM bytes = 2 x "
-                     "FETCH_SIZE (gfx950 counts wide streaming reads at half) + WRITE_SIZE, KB units; algorithmic = "
-                     "dY and X operands (bf16) once + dW (fp32) once per block in the group",
-           "launches": out}
-    res["algorithmic_bytes_per_launch"] = round(sum(o["algorithmic_bytes"] for o in out) / len(out))
+                     "FETCH_SIZE (gfx950 counts wide streaming reads at half) + WRITE_SIZE, KB units, averaged over "
+                     "every launch of the class"}
+    if probe == "gemm_dw_grouped":
+        per_block, dw_block = dw_block_bytes(c)
+        for o in out:
+            o["blocks"] = max(1, round(o["write_bytes"] / dw_block))
+            o["algorithmic_bytes"] = o["blocks"] * per_block
+        res["algorithmic_bytes_per_launch"] = round(sum(o["algorithmic_bytes"] for o in out) / len(out))
+        res["algorithmic_source"] = "dY and X operands (bf16) once + dW (fp32) once per block in the group"
+    else:
+        b = json.loads(Path(bench_json).read_text())
+        assert b["roofline"]["kernel"] == probe, b["roofline"]["kernel"]
+        res["algorithmic_bytes_per_launch"] = b["roofline"]["algorithmic_bytes_per_launch"]
+        res["algorithmic_source"] = f"{bench_json}: roofline.algorithmic_bytes_per_launch (library probe)"
     res["ratio"] = round(res["hbm_bytes_per_launch"] / res["algorithmic_bytes_per_launch"], 3)
-    dst = ROOT / "profiles" / "round2" / f"pmc_traffic_{cfg}.json"
+    res["launches"] = out
+    dst = ROOT / "profiles" / rnd / f"pmc_traffic_{cfg}_{probe}.json"
+    dst.parent.mkdir(parents=True, exist_ok=True)
     dst.write_text(json.dumps(res, indent=1) + "\n")
-    print(dst, res["hbm_bytes_per_launch"], res.get("ratio"))
+    print(dst, res["hbm_bytes_per_launch"], res["algorithmic_bytes_per_launch"], res["ratio"])
 
 
 if __name__ == "__main__":
