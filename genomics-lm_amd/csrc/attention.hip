@@ -13,6 +13,7 @@
 //                    fp32 or bf16 storage.  Used for the fp32 parity mode and as the
 //                    bf16 fallback for head dims the MFMA kernel does not cover.
 //   * attn_*_mfma  : bf16 MFMA 32x32x16 kernels (hd in {32, 48, 64}) -- attention_mfma.h
+//   * attn_fwd_f32mfma : the fp32 forward on f32 MFMA (hd % 8 == 0, hd <= 64) -- attention_f32.h
 #include "common.h"
 
 constexpr int AV_HD = 64;   // max head dim of the vector kernels
@@ -282,6 +283,7 @@ __global__ __launch_bounds__(64) void attn_bwd_dkdv_vec(const T* __restrict__ qk
 }
 
 #include "attention_mfma.h"
+#include "attention_f32.h"
 
 // ---------------------------------------------------------------------------
 // Attention probabilities of one layer, materialised (the manual path's `last_attn`,
@@ -363,6 +365,9 @@ extern "C" int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const in
     return attn_fwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (bf16_t*)y, ldy, lse, B, T, H, KV, hd, window,
                                 drop_seed, thr, dscale, scale, (const uint32_t*)drop_mask, s);
   }
+  if (dtype != CG_BF16 && attn_f32mfma_supported(hd, qkv, ldqkv, y, ldy))
+    return attn_fwd_f32mfma_launch((const float*)qkv, ldqkv, segstart, (float*)y, ldy, lse, B, T, H, KV, hd, window,
+                                   drop_seed, thr, dscale, scale, s);
   dim3 g(cg_cdiv(T, AV_TQ), B * H);
   if (dtype == CG_BF16)
     hipLaunchKernelGGL(attn_fwd_vec<bf16_t>, g, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart, (bf16_t*)y,

@@ -156,6 +156,100 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// fp32 kernel for K-contiguous operands (the parity-mode forward and every product whose
+// operands are row-major in K): 128x128x16 tile, 4 waves of 64x64, v_mfma_f32_32x32x2_f32 (an
+// exact fp32 fma chain at 64 FLOP/clk/SIMD).  Operands are register-staged 16-B chunks into a
+// double-buffered [128 rows][16 k] image per operand whose 16-B chunks are XOR-swizzled by
+// (row >> 2) & 3, so the fragment reads (one ds_read_b128 per 4 MFMA k-steps: half-wave h takes
+// k = 8g + 4h + t at k-step 4g + t) are conflict-free.  The contraction order differs from the
+// 64x64 kernel's (fp32 rounding differences only).
+// ---------------------------------------------------------------------------
+namespace f32b {
+constexpr int BM = 128, BN = 128, BKT = 16;
+constexpr int IMG = BM * BKT * 4;  // 8 KiB per operand image
+__device__ __forceinline__ int off(int row, int ch) { return row * 64 + 16 * (ch ^ ((row >> 2) & 3)); }
+}  // namespace f32b
+
+__global__ __launch_bounds__(256) void gemm_f32_big_kernel(GemmParams p) {
+  using namespace f32b;
+  __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hl = lane >> 5;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int kbeg = blockIdx.z * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const float* A = (const float*)p.A;
+  const float* B = (const float*)p.B;
+  v16f acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  float4 sa[2], sb[2];
+  auto load = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i, row = c >> 2, k = k0 + 4 * (c & 3);
+      const int m = m0 + row, n = n0 + row;
+      sa[i] = (m < p.M && k < kend) ? *(const float4*)(A + (long long)m * p.lda + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      sb[i] = (n < p.N && k < kend) ? *(const float4*)(B + (long long)n * p.ldb + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](char* img) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int c = tid + 256 * i;
+      *(float4*)(img + off(c >> 2, c & 3)) = sa[i];
+      *(float4*)(img + IMG + off(c >> 2, c & 3)) = sb[i];
+    }
+  };
+  // per-lane fragment offsets: row (l & 31) of a 32-row block, chunk 2g + hl
+  const int ao[2] = {off(lane & 31, hl), off(lane & 31, 2 + hl)};
+  load(kbeg);
+  store(smem);
+  __syncthreads();
+  int cur = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += BKT) {
+    const bool more = k0 + BKT < kend;
+    if (more) load(k0 + BKT);
+    const char* img = smem + cur * 2 * IMG;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      float4 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = *(const float4*)(img + (wm + 32 * i) * 64 + ao[g]);
+        b[i] = *(const float4*)(img + IMG + (wn + 32 * i) * 64 + ao[g]);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+        }
+    }
+    if (more) store(smem + (cur ^ 1) * 2 * IMG);  // last read before the previous barrier
+    __syncthreads();
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int col = n0 + wn + 32 * j + (lane & 31);
+        epi_store(p, row, col, acc[i][j][r], blockIdx.z);
+      }
+}
+
+// ---------------------------------------------------------------------------
 // bf16 kernel: 128x128x64, 16x16x32 bf16 MFMA
 // ---------------------------------------------------------------------------
 namespace bfg {
@@ -526,6 +620,11 @@ struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC
 // whole C4 step measured 8.45 vs 8.41 ms (bench.py, 2 x 2 interleaved runs on one box) -- so it
 // is off by default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
 // products without an epilogue or with a bias only, 2 for every epilogue it implements.
+// CG_F32_BIG=0 routes K-contiguous fp32 products back to the 64x64 kernel (A/B switch)
+static int g_f32_big = [] {
+  const char* e = getenv("CG_F32_BIG");
+  return e ? atoi(e) : 1;
+}();
 static int g_pers_lw = [] {
   const char* e = getenv("CG_PERS_LW");
   return e ? atoi(e) : 0;
@@ -703,9 +802,15 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
 
   if (d->in_dtype == CG_F32) {
     p.epi &= ~CG_EPI_COLSUM;
-    dim3 g(cg_cdiv(p.N, 64), cg_cdiv(p.M, 64), split);
-    launch4(gemm_f32_kernel<false, false>, gemm_f32_kernel<false, true>, gemm_f32_kernel<true, false>,
-            gemm_f32_kernel<true, true>, d->a_kcontig, d->b_kcontig, g, dim3(256), 0, s, p);
+    if (d->a_kcontig && d->b_kcontig && !(d->lda & 3) && !(d->ldb & 3) && !(d->K & 3) &&
+        !((uintptr_t)d->A & 15) && !((uintptr_t)d->B & 15) && g_f32_big) {
+      hipLaunchKernelGGL(gemm_f32_big_kernel, dim3(cg_cdiv(p.N, f32b::BN), cg_cdiv(p.M, f32b::BM), split), dim3(256),
+                         0, s, p);
+    } else {
+      dim3 g(cg_cdiv(p.N, 64), cg_cdiv(p.M, 64), split);
+      launch4(gemm_f32_kernel<false, false>, gemm_f32_kernel<false, true>, gemm_f32_kernel<true, false>,
+              gemm_f32_kernel<true, true>, d->a_kcontig, d->b_kcontig, g, dim3(256), 0, s, p);
+    }
   } else if (d->in_dtype == CG_BF16) {
     if ((d->lda & 7) || (d->ldb & 7)) return CG_EUNSUPPORTED;
     if (((uintptr_t)d->A & 15) || ((uintptr_t)d->B & 15)) return CG_EUNSUPPORTED;
