@@ -20,7 +20,7 @@ SIG = {
     "cg_attn_drop_mask": (i32, [i32, i32, i32, u32, f32, vp, vp]),
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
-                          u32, f32, vp, vp, i64, vp, vp]),
+                          u32, f32, vp, vp, i64, vp, sz, vp]),
 }
 BF16 = 1
 
