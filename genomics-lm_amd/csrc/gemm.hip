@@ -617,8 +617,9 @@ struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC
 // interleaved on one box) it takes qkv dX 28.3 -> 26.9 us and fc1 dX 35.0 -> 32.7 us (qkv fwd
 // and proj dX unchanged), while the VALU- and memory-heavy epilogues (GELU, dGELU + column sums,
 // fp32 residual) run 1.2-2.3 us slower in it; with it on the plain / bias-only products the
-// whole C4 step measured 8.45 vs 8.41 ms (bench.py, 2 x 2 interleaved runs on one box) -- so it
-// is off by default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
+// whole C4 step measured 8.45 vs 8.41 ms on one box (bench.py, 2 x 2 interleaved runs) but
+// 7.971 vs 8.034 and 8.05 vs 8.12 ms on two later boxes (3 x 2 and 2 x 3 interleaved runs, round 3):
+// mode 1 is the default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
 // products without an epilogue or with a bias only, 2 for every epilogue it implements.
 // CG_F32_BIG=0 routes K-contiguous fp32 products back to the 64x64 kernel (A/B switch)
 static int g_f32_big = [] {
@@ -627,7 +628,7 @@ static int g_f32_big = [] {
 }();
 static int g_pers_lw = [] {
   const char* e = getenv("CG_PERS_LW");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : 1;
 }();
 extern "C" int cg_gemm_set_pers_lw(int mode) {
   const int old = g_pers_lw;

@@ -85,8 +85,8 @@ int cg_gemm_set_pers(int mode);
  * (CU count - reserve) workgroups; env CG_PERS_CU_RESERVE sets it at load.  Returns the previous
  * reserve.  cg_pers_cus: the CU count those launches (and the dW planner) use now. */
 int cg_set_cu_reserve(int n);
-/* persistent-tile variant with dedicated LDS-DMA loader waves (gemm_lw.h): 0 off (default; env
- * CG_PERS_LW at load), 1 for products without an epilogue or with a bias only, 2 wherever it
+/* persistent-tile variant with dedicated LDS-DMA loader waves (gemm_lw.h): 0 off, 1 (default; env
+ * CG_PERS_LW at load) for products without an epilogue or with a bias only, 2 wherever it
  * implements the epilogue.  Returns the previous mode. */
 int cg_gemm_set_pers_lw(int mode);
 int cg_pers_cus(void);

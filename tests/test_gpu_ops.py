@@ -553,7 +553,7 @@ def test_transpose16_batch():
         assert torch.equal(o.cpu(), m.cpu().t())
 
 
-@pytest.mark.parametrize("lw", [0, 2])
+@pytest.mark.parametrize("lw", [0, 1, 2])
 @pytest.mark.parametrize("cap", [1, 3])
 @pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256), (600, 200, 320),
                                    (520, 264, 512)])
