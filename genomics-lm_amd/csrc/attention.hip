@@ -379,7 +379,8 @@ extern "C" int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const in
   return CG_OK;
 }
 
-extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return (size_t)B * H * T * sizeof(float); }
+// delta (the vector path's rowsum(dO o O); the MFMA path's nd = -delta/dscale) | -lse2 (MFMA path)
+extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return 2 * (size_t)B * H * T * sizeof(float); }
 
 extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const void* y,
                            long long ldy, const void* dy, long long lddy, const float* lse, void* dqkv,

@@ -66,6 +66,20 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, uint32_t lds, ui
       : "memory");
 }
 __device__ __forceinline__ void dma_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// one dword per lane into LDS at lds + 4 * lane (a 64-entry row of per-query values)
+__device__ __forceinline__ void dma4(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dword %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds), "s"(r)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void dma_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 struct TileDma {
   __amdgpu_buffer_rsrc_t r;
@@ -565,7 +579,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
                                                            const bf16_t* __restrict__ dy, long long lddy,
                                                            const bf16_t* __restrict__ yo, long long ldy,
                                                            const float* __restrict__ lse,
-                                                           float* __restrict__ delta, bf16_t* __restrict__ dqkv,
+                                                           float* __restrict__ delta, float* __restrict__ nlse2,
+                                                           bf16_t* __restrict__ dqkv,
                                                            long long lddq, int T, int H, int KV, int hd_rt, int window,
                                                            uint32_t seed, uint32_t thr, float dscale, float scale,
                                                            const uint32_t* __restrict__ qmask, int wpr,
@@ -598,7 +613,12 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
   const float c = scale * 1.4426950408889634f;
   const float lse2 = qok ? lse[bhq] * 1.4426950408889634f : 0.f;
   const float dl = dpart + __shfl_xor(dpart, 32, 64);
-  if (qok && lane < 32) delta[bhq] = dl;
+  // for the dK/dV kernel's row DMAs, in the form its accumulators start from: nd = -delta/dscale
+  // (the dP start) and -lse2 (the S start)
+  if (qok && lane < 32) {
+    delta[bhq] = -dl * (DROP ? 1.0f / dscale : 1.0f);
+    nlse2[bhq] = -lse2;
+  }
   const int lo = qok ? lo_of(seg, rowbase, myq, T, window) : 0x7fffffff;
   const int kmin = lo_of(seg, rowbase, q0, T, window);
   const int kmax = min(T - 1, q0 + 127);
@@ -763,6 +783,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
                                                              const bf16_t* __restrict__ dy, long long lddy,
                                                              const float* __restrict__ lse,
                                                              const float* __restrict__ delta,
+                                                             const float* __restrict__ nlse2,
                                                              bf16_t* __restrict__ dqkv, long long lddq, int T, int H,
                                                              int KV, int hd_rt, int window, uint32_t seed, uint32_t thr,
                                                              float dscale, float scale,
@@ -774,7 +795,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // per buffer: Q image | dO image | lse2[64] | delta[64] | lo[64] | rowhash[64]
   //             (+ DROP 2: the keep words of the tile's 64 queries x 128 keys, [key word][query])
-  constexpr int BUF = 2 * IMG + 4 * 64 * 4 + (DROP == 2 ? 4 * 64 * 4 : 0);
+  //             | a 64-word slot wave 3's row DMA fills (keeps every wave's DMA count equal)
+  constexpr int BUF = 2 * IMG + 4 * 64 * 4 + (DROP == 2 ? 4 * 64 * 4 : 0) + 64 * 4;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int bk = blockIdx.x, b = bk / KV, kvh = bk % KV;
   const int rep = H / KV;
@@ -795,7 +817,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     vf[ks] = frag_global(vrow, kok, ks, hd, lane);
   }
   // dS is accumulated divided by the dropout scale (see nd): dK = kscale * (Q^T . dS/dscale)
-  const float ndscale = DROP ? 1.0f / dscale : 1.0f;
   const float kscale = DROP ? scale * dscale : scale;
   constexpr int nks = (hd + 15) >> 4;
   const uint32_t kcol = ((uint32_t)mykey >> 1) * CG_COLK;
@@ -809,57 +830,65 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   const int qt_end = (qend - 1) / KT;  // inclusive
   const int nqt = qt_end - qt_begin + 1;
   const int total = nqt * rep;
-  // the per-query rows (lse, delta, segment start) are prefetched with the tiles: loading
-  // them at store time would expose a global-memory round trip every iteration
-  float pl = 0.f, pdl = 0.f;
-  int plo = 0x7fffffff;
-  // keep words of (query head, query tile): thread tid fetches query tid&63's word for keys
-  // kt0 + 32(tid>>6) .. +31 with the tiles
-  uint32_t wn = 0;
-  const int mw_idx = kt0 / 32 + (tid >> 6);
+  // Three LDS buffers: everything iteration it+2 reads -- the Q / dO images and the per-query rows
+  // (-lse2 and nd, both written by the dQ kernel; segment starts; keep words) -- streams in by
+  // LDS-DMA while iteration it computes, so the wait at the end of iteration it (a counted vmcnt
+  // that leaves the newest iteration's DMAs in flight) is for data issued one iteration earlier.
+  // Per wave and iteration: 4 image pieces + 1 row (wave 0: -lse2, 1: nd, 2: segment starts,
+  // 3: the segment starts again, into a slot of its own that nothing reads)
+  // + (DROP == 2) its 64 keep words.
+  constexpr int NBUF = 3;
+  constexpr int NV = 5 + (DROP == 2 ? 1 : 0);
+  const int mw_idx = kt0 / 32 + wave;  // this wave's key word of a query's keep bits
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
   const TileDma qsrc = tile_dma_src(qkv + rowbase * ld, ld, T, hd, wave_u, lane);
   const TileDma dsrc = tile_dma_src(dy + rowbase * lddy, lddy, T, hd, wave_u, lane);
   const uint32_t qstride = (uint32_t)(KT * ld * 2), dstride = (uint32_t)(KT * lddy * 2);
+  constexpr uint32_t OORD = 0x80000000u;  // past every record: the DMA writes 0
+  const long long bh0 = (long long)b * H * T;  // (b, head 0, query 0) of the per-query rows
+  const float* rowsrc = wave_u == 0 ? nlse2 : delta;
+  const __amdgpu_buffer_rsrc_t rrow =
+      wave_u < 2 ? __builtin_amdgcn_make_buffer_rsrc((void*)(rowsrc + bh0), (short)0, H * T * 4, 0x00020000)
+                 : __builtin_amdgcn_make_buffer_rsrc((void*)(seg ? seg + rowbase : nullptr), (short)0,
+                                                     seg ? T * 4 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rqm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(DROP == 2 ? qmask + bh0 * wpr : nullptr), (short)0, DROP == 2 ? H * T * wpr * 4 : 0, 0x00020000);
+  const uint32_t row_lds = (uint32_t)(wave_u < 3 ? 2 * IMG + wave_u * 64 * 4 : BUF - 64 * 4);  // -lse2 | nd | seg
   // iteration cursor: (query head, query tile), advanced without divisions
   struct Cur { int h2, qt; };
   auto next_of = [&](Cur c) { return c.qt < qt_end ? Cur{c.h2, c.qt + 1} : Cur{c.h2 + 1, qt_begin}; };
-  // the images go straight to LDS buffer `nb`; the per-query rows through registers
-  auto stage_load = [&](Cur cu, int nb) {
+  auto stage_dma = [&](Cur cu, int nb) {
     const int h2 = cu.h2, qt = cu.qt;
-    tile_dma(lds0 + nb * BUF, qsrc, qt * qstride + (uint32_t)(h2 * hd * 2), wave_u);
-    tile_dma(lds0 + nb * BUF + IMG, dsrc, qt * dstride + (uint32_t)(h2 * hd * 2), wave_u);
-    if constexpr (DROP == 2) {
-      const int q = qt * KT + (tid & 63);
-      wn = (q < T && mw_idx < wpr) ? qmask[(((long long)b * H + h2) * T + q) * wpr + mw_idx] : 0u;
-    }
-    if (tid < 64) {
-      const int q = qt * KT + tid;
-      const long long bhq = ((long long)b * H + h2) * T + (q < T ? q : 0);
-      pl = q < T ? lse[bhq] : 0.f;
-      pdl = q < T ? delta[bhq] : 0.f;
-      plo = q < T ? lo_of(seg, rowbase, q, T, window) : 0x7fffffff;
-    }
+    const uint32_t buf = lds0 + nb * BUF;
+    tile_dma(buf, qsrc, qt * qstride + (uint32_t)(h2 * hd * 2), wave_u);
+    tile_dma(buf + IMG, dsrc, qt * dstride + (uint32_t)(h2 * hd * 2), wave_u);
+    const int q = qt * KT + lane;
+    dma4(rrow, buf + row_lds, q < T ? (uint32_t)(((wave_u < 2 ? h2 * T : 0) + q) * 4) : OORD);
+    if constexpr (DROP == 2)
+      dma4(rqm, buf + (uint32_t)(2 * IMG + 4 * 64 * 4 + wave_u * 64 * 4),
+           (q < T && mw_idx < wpr) ? (uint32_t)(((h2 * T + q) * wpr + mw_idx) * 4) : OORD);
   };
-  auto stage_store = [&](Cur cu, char* buf) {
-    if (tid < 64) {
-      const int h2 = cu.h2, qt = cu.qt;
-      const int q = qt * KT + tid;
-      float* fl = (float*)(buf + 2 * IMG);
-      int* il = (int*)(buf + 2 * IMG + 2 * 64 * 4);
-      fl[tid] = -pl * 1.4426950408889634f;  // -lse2: the S accumulator's start
-      fl[64 + tid] = -pdl * ndscale;  // nd = -delta / dscale: the dP accumulator's start
-      il[tid] = plo;
-      il[64 + tid] = DROP == 1 ? (int)cg_row_hash(seed, (uint32_t)(((long long)b * H + h2) * T + q)) : 0;
+  // DROP == 1: the row hashes of cu into its buffer's hash slot (after that buffer's DMAs landed)
+  auto stage_hash = [&](Cur cu, char* bufp) {
+    if constexpr (DROP == 1) {
+      if (tid < 64)
+        ((uint32_t*)(bufp + 2 * IMG + 3 * 64 * 4))[tid] =
+            cg_row_hash(seed, (uint32_t)(((long long)b * H + cu.h2) * T + cu.qt * KT + tid));
     }
-    if constexpr (DROP == 2) ((uint32_t*)(buf + 2 * IMG + 4 * 64 * 4))[tid] = wn;
   };
   Cur cur{kvh * rep, qt_begin};
+  Cur n1 = next_of(cur);
+  Cur n2 = next_of(n1);
   if (total > 0) {
-    stage_load(cur, 0);
-    stage_store(cur, smem);
-    dma_drain();
+    stage_dma(cur, 0);
+    if (total > 1) {
+      stage_dma(n1, 1);
+      dma_wait<NV>();
+    } else {
+      dma_wait<0>();
+    }
+    stage_hash(cur, smem);
   }
   __syncthreads();
   const RowOff ro = row_offsets(lane);
@@ -874,15 +903,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     const float* nds = lse2s + 64;
     const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
     const uint32_t* hrs = (const uint32_t*)(buf + 2 * IMG + 3 * 64 * 4);
-    const bool more = it + 1 < total;
+    const bool more1 = it + 1 < total, more2 = it + 2 < total;
     // this wave's key word of the tile's keep bits, [query]
     const uint32_t* mws = (const uint32_t*)(buf + 2 * IMG + 4 * 64 * 4) + wave * 64;
-    const Cur nx = next_of(cur);
-    if (more) stage_load(nx, CUR ^ 1);  // that buffer was last read before the previous barrier
+    if (more2) stage_dma(n2, (CUR + 2) % NBUF);  // that buffer was last read before the previous barrier
     const int q0 = cur.qt * KT;
     // wave activity: some query q in [q0, q0+63] sees some key in [kw0, kw0+31]
     const int qlast = min(T - 1, q0 + KT - 1);
-    const bool active = (qlast >= kw0) && (los[0] <= kw0 + 31);
+    // segment start of query q0 + i raised by the local window (the rows hold the raw segment starts)
+    auto lo_at = [&](int i) { return window > 0 ? max(los[i], q0 + i - window + 1) : los[i]; };
+    const bool active = (qlast >= kw0) && (lo_at(0) <= kw0 + 31);
     // full: every (query, key) of the wave's tile visible.  Otherwise the invisible scores are
     // set to -inf before the exponent (the branch touches only s: the dK/dV accumulators keep
     // their registers across it)
@@ -920,7 +950,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int q = q0 + qi + u;
-              s[rg + u] = ((mykey > q) | (mykey < lov[u]) | (q >= T)) ? -INFINITY : s[rg + u];
+              const int lq = window > 0 ? max(lov[u], q - window + 1) : lov[u];
+              s[rg + u] = ((mykey > q) | (mykey < lq) | (q >= T)) ? -INFINITY : s[rg + u];
             }
           }
         }
@@ -971,16 +1002,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         ATTN_SETPRIO(0);
       }
     };
-    if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (los[qlast - q0] <= kw0));
-    if (more) stage_store(nx, smem + (CUR ^ 1) * BUF);
-    cur = nx;
-    dma_drain();
-    __syncthreads();
+    if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0));
+    if (more1) {  // n1's data (issued an iteration ago) landed; n2's DMAs may still be in flight
+      if (more2) dma_wait<NV>();
+      else dma_wait<0>();
+      stage_hash(n1, smem + ((CUR + 1) % NBUF) * BUF);
+    }
+    cur = n1;
+    n1 = n2;
+    n2 = next_of(n2);
+    // raw barrier: no vmcnt(0) (n2's DMAs stay in flight); the row stores and this wave's image
+    // reads retired first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   };
-  for (int it = 0; it < total; it += 2) {
+  for (int it = 0; it < total; it += NBUF) {
     iter(std::integral_constant<int, 0>{}, it);
     if (it + 1 < total) iter(std::integral_constant<int, 1>{}, it + 1);
+    if (it + 2 < total) iter(std::integral_constant<int, 2>{}, it + 2);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the loop
   if (kok) {
     bf16_t* kr = dqkv + (rowbase + mykey) * lddq + koff;
     bf16_t* vr = dqkv + (rowbase + mykey) * lddq + voff;
@@ -1073,6 +1115,7 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
                                        const uint32_t* dmask, float* bpart, long long ldp, hipStream_t s) {
   dim3 gq(B * H, cg_cdiv(T, 128));
   const int wpr = attn_drop_wpr(T);
+  float* nlse2 = delta + (long long)B * H * T;  // second half of the workspace
   const int mode = thr ? (dmask ? 2 : 1) : 0;
   const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
   // the K/V ring, or the bias-partial reduction buffer when it is larger
@@ -1080,7 +1123,7 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_begin(CG_PROBE_ATTN_DQ, s);
 #define DQ(D, HDv)                                                                                             \
   hipLaunchKernelGGL((attn_bwd_dq_mfma<D, HDv>), gq, dim3(256), shq, s, qkv, ld, seg, dy, lddy, y, ldy, lse, \
-                     delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
+                     delta, nlse2, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
 #define DQH(D) if (hd == 64) DQ(D, 64); else if (hd == 48) DQ(D, 48); else DQ(D, 32)
   if (mode == 2) { DQH(2); } else if (mode == 1) { DQH(1); } else { DQH(0); }
 #undef DQH
@@ -1088,11 +1131,11 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_end(CG_PROBE_ATTN_DQ, s, 3.0 * tri);  // S, dP recomputed + dQ
   CG_LAUNCH_CHECK();
   dim3 gk(B * KV, cg_cdiv(T, 128));
-  const size_t shk = std::max<size_t>(2 * (2 * fa::IMG + 4 * 64 * 4 + (mode == 2 ? 4 * 64 * 4 : 0)),
+  const size_t shk = std::max<size_t>(3 * (2 * fa::IMG + 5 * 64 * 4 + (mode == 2 ? 4 * 64 * 4 : 0)),
                                       bpart ? fa::COLSUM_LDS : 0);
   cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
 #define DKDV(D, HDv)                                                                                            \
-  hipLaunchKernelGGL((attn_bwd_dkdv_mfma<D, HDv>), gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv,  \
+  hipLaunchKernelGGL((attn_bwd_dkdv_mfma<D, HDv>), gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, nlse2, dqkv, \
                      lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
 #define DKH(D) if (hd == 64) DKDV(D, 64); else if (hd == 48) DKDV(D, 48); else DKDV(D, 32)
   if (mode == 2) { DKH(2); } else if (mode == 1) { DKH(1); } else { DKH(0); }

@@ -107,12 +107,14 @@ __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)
 __device__ __forceinline__ float gelu_phi_q(float x, float& e) {
   e = __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);  // e^{-x^2/2}
   const float t = __builtin_amdgcn_rcpf(fmaf(0.23164189992f, fabsf(x), 1.0f));  // p/sqrt(2) = 0.3275911/1.41421
-  float poly = fmaf(t, 1.061405429f, -1.453152027f);
-  poly = fmaf(t, poly, 1.421413741f);
-  poly = fmaf(t, poly, -0.284496736f);
-  poly = fmaf(t, poly, 0.254829592f);
-  const float q = 0.5f * t * poly * e;  // = 0.5 * erfc(|x|/sqrt2)
-  return x >= 0.f ? 1.0f - q : q;       // Phi(x)
+  // the A&S polynomial with its coefficients times -1/2: h = 0.5 - 0.5 erfc(|x|/sqrt2) in one fma
+  float poly = fmaf(t, -0.5307027145f, 0.7265760135f);
+  poly = fmaf(t, poly, -0.7107068705f);
+  poly = fmaf(t, poly, 0.142248368f);
+  poly = fmaf(t, poly, -0.127414796f);
+  const float h = fmaf(t * poly, e, 0.5f);  // = 1/2 - q, q = 0.5 * erfc(|x|/sqrt2)
+  // Phi(x) = 1/2 + sign(x) h (h >= 0): the sign bit of x copied onto h, one v_bfi
+  return 0.5f + __uint_as_float((__float_as_uint(h) & 0x7FFFFFFFu) | (__float_as_uint(x) & 0x80000000u));
 }
 __device__ __forceinline__ float gelu_fast(float x) {
   float e;

@@ -190,6 +190,15 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
   auto epilogue = [&](int k) __attribute__((always_inline)) {
     int m0, n0;
     tile_org(k, m0, n0);
+    // alpha != 1 (the tied head's scaled gradient) is rare: a real branch (the empty volatile asm
+    // keeps hipcc from if-converting it into 64 selects per tile on every epilogue)
+    if (__builtin_expect(scaled, 0)) {
+      asm volatile("");
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] *= p.alpha;
+    }
     int col[2];
     uint32_t off_c[4][2];
 #pragma unroll
@@ -272,10 +281,6 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
         for (int h = 0; h < 2; ++h)
 #pragma unroll
           for (int u = 0; u < 4; ++u) v[4 * h + u] = acc[i][2 * c + h][u];
-        if (scaled) {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] *= p.alpha;
-        }
         if constexpr ((EPI & CG_EPI_BIAS) != 0) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += bia[c][j];
