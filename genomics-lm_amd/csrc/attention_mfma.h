@@ -31,6 +31,10 @@
 #ifndef ATTN_PRIO
 #define ATTN_PRIO 0
 #endif
+// timing-only diagnostic: the forward and dQ kernels skip the per-tile DMA drain
+#ifndef ATTN_DIAG_NODRAIN
+#define ATTN_DIAG_NODRAIN 0
+#endif
 #if ATTN_PRIO
 #define ATTN_SETPRIO(x) __builtin_amdgcn_s_setprio(x)
 #else
@@ -538,7 +542,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       if ((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max)) body(Ki, Vi, k0, wc, std::true_type{});
       else body(Ki, Vi, k0, wc, std::false_type{});
     }
-    dma_drain();
+    if (!ATTN_DIAG_NODRAIN) dma_drain();  // diagnostic builds only (results invalid)
     __syncthreads();
   };
   for (int t = t0; t <= t1; t += 2) {
@@ -737,7 +741,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
       }
     };
     if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) body((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max));
-    dma_drain();
+    if (!ATTN_DIAG_NODRAIN) dma_drain();  // diagnostic builds only (results invalid)
     __syncthreads();
   };
   for (int t = t0; t <= t1; t += 2) {
