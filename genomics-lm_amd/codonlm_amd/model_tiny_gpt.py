@@ -297,11 +297,16 @@ class TinyGPT(nn.Module):
         return mod, parts[-1]
 
     def _bind_views(self):
+        pairs = []
         for name, spec in self._specs.items():
             mod, attr = self._param_by_name(name)
             p = getattr(mod, attr)
             p.data = self._view(self._flat, spec)
-            p.grad = self._view(self._flat_grad, spec)
+            g = self._view(self._flat_grad, spec)
+            p.grad = g
+            pairs.append((p, g))
+        # (parameter, its view of the flat grad buffer): re-attached by _bind_grad_views
+        self._grad_pairs = pairs
 
     @torch.no_grad()
     def _reference_init(self):
@@ -393,9 +398,13 @@ class TinyGPT(nn.Module):
         self._bind_grad_views()
 
     def _bind_grad_views(self):
-        for name, spec in self._specs.items():
-            mod, attr = self._param_by_name(name)
-            getattr(mod, attr).grad = self._view(self._flat_grad, spec)
+        # runs twice per microbatch (zero_grad, after the backward): only grads that something
+        # replaced or set to None are re-attached -- re-creating and re-assigning every view took
+        # milliseconds of host time per step and left the GPU idle between optimizer step and
+        # the next forward
+        for p, g in self._grad_pairs:
+            if p.grad is not g:
+                p.grad = g
 
     def _native_backward(self, gout, d_term=None, d_offsets=None):
         """Native backward of the last forward: ``gout`` = d(objective)/d(loss) (None when the

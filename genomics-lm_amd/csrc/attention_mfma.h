@@ -275,6 +275,30 @@ __device__ __forceinline__ v16f zero16() {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// One 32-row accumulator block x (lane: the query / key l&31; element r: head dim acc_row(r)),
+// times sc, stored as bf16 from d = 0 of the block at row pointer rowp, nd valid dims (a multiple
+// of 16).  Groups j = r/4 hold dims 8j + 4(l>>5) + 0..3; one v_permlane32_swap per dword of each
+// group pair (j, j+1) leaves lanes 0-31 with dims 8j..8j+7 and lanes 32-63 with 8j+8..8j+15, so
+// the block takes two 16-byte stores per lane instead of four 8-byte ones (T21).  Every lane
+// takes part in the swaps; `ok` only predicates the stores.
+__device__ __forceinline__ void store_blk16(bf16_t* rowp, const v16f& x, float sc, bool ok, int nd, int lane) {
+  const int hl = lane >> 5;
+#pragma unroll
+  for (int jp = 0; jp < 4; jp += 2) {
+    uint32_t a[2], b[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a[h] = pk2bf(x[4 * jp + 2 * h] * sc, x[4 * jp + 2 * h + 1] * sc);
+      b[h] = pk2bf(x[4 * (jp + 1) + 2 * h] * sc, x[4 * (jp + 1) + 2 * h + 1] * sc);
+      const auto r = __builtin_amdgcn_permlane32_swap(a[h], b[h], false, false);
+      a[h] = r[0];
+      b[h] = r[1];
+    }
+    const int d = 8 * jp + 8 * hl;
+    if (ok && 8 * jp + 16 <= nd) *(uint4*)(rowp + d) = make_uint4(a[0], a[1], b[0], b[1]);
+  }
+}
+
 // Column sums over the workgroup's 128 accumulator columns (4 waves x 32 lanes) of the 64 rows
 // held in two accumulator blocks x0 (rows 0..31) and x1 (32..63), for the bias-gradient partials:
 // the values go through LDS ([wave][row][33 lanes], conflict-free stores and reads), each thread
@@ -550,25 +574,13 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
     if (t + 1 <= t1) step(std::integral_constant<int, 1>{}, t + 1);
   }
   const float ltot = ls[0];
-  if (qok) {
+  {
     const float inv = (DROP ? dscale : 1.0f) / ltot;
-    bf16_t* yr = y + (rowbase + myq) * ldy + (long long)hh * hd;
-#pragma unroll
-    for (int r = 0; r < 16; r += 4) {
-      const int d0 = acc_row(r, lane);
-      if (d0 < hd) {
-        uint2 w;
-        w.x = (uint32_t)f2bf(o0[r] * inv) | ((uint32_t)f2bf(o0[r + 1] * inv) << 16);
-        w.y = (uint32_t)f2bf(o0[r + 2] * inv) | ((uint32_t)f2bf(o0[r + 3] * inv) << 16);
-        *(uint2*)(yr + d0) = w;
-      }
-      if (d0 + 32 < hd) {
-        uint2 w;
-        w.x = (uint32_t)f2bf(o1[r] * inv) | ((uint32_t)f2bf(o1[r + 1] * inv) << 16);
-        w.y = (uint32_t)f2bf(o1[r + 2] * inv) | ((uint32_t)f2bf(o1[r + 3] * inv) << 16);
-        *(uint2*)(yr + d0 + 32) = w;
-      }
-    }
+    bf16_t* yr = y + (rowbase + (qok ? myq : 0)) * ldy + (long long)hh * hd;
+    store_blk16(yr, o0, inv, qok, hd < 32 ? hd : 32, lane);
+    if (hd > 32) store_blk16(yr + 32, o1, inv, qok, hd - 32, lane);
+  }
+  if (qok) {
     if (hl == 0) lse[((long long)b * H + hh) * T + myq] = m * scale + __logf(ltot);
   }
 }
@@ -750,24 +762,10 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
   }
   // dQ = qscale * (dS/dscale . K)
   const float qscale = DROP ? scale * dscale : scale;
-  if (qok) {
-    bf16_t* dr = dqkv + (rowbase + myq) * lddq + (long long)hh * hd;
-#pragma unroll
-    for (int r = 0; r < 16; r += 4) {
-      const int d0 = acc_row(r, lane);
-      if (d0 < hd) {
-        uint2 w;
-        w.x = (uint32_t)f2bf(a0[r] * qscale) | ((uint32_t)f2bf(a0[r + 1] * qscale) << 16);
-        w.y = (uint32_t)f2bf(a0[r + 2] * qscale) | ((uint32_t)f2bf(a0[r + 3] * qscale) << 16);
-        *(uint2*)(dr + d0) = w;
-      }
-      if (d0 + 32 < hd) {
-        uint2 w;
-        w.x = (uint32_t)f2bf(a1[r] * qscale) | ((uint32_t)f2bf(a1[r + 1] * qscale) << 16);
-        w.y = (uint32_t)f2bf(a1[r + 2] * qscale) | ((uint32_t)f2bf(a1[r + 3] * qscale) << 16);
-        *(uint2*)(dr + d0 + 32) = w;
-      }
-    }
+  {
+    bf16_t* dr = dqkv + (rowbase + (qok ? myq : 0)) * lddq + (long long)hh * hd;
+    store_blk16(dr, a0, qscale, qok, hd < 32 ? hd : 32, lane);
+    if (hd > 32) store_blk16(dr + 32, a1, qscale, qok, hd - 32, lane);
   }
   if (bpart) {  // q-bias gradient partial: column sums of this workgroup's dQ rows (fp32)
     const float v = colsum_wg(a0, a1, qscale, qok, (float*)smem, wave, lane, tid);  // the ring is idle
@@ -1027,31 +1025,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     if (it + 2 < total) iter(std::integral_constant<int, 2>{}, it + 2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the loop
-  if (kok) {
-    bf16_t* kr = dqkv + (rowbase + mykey) * lddq + koff;
-    bf16_t* vr = dqkv + (rowbase + mykey) * lddq + voff;
+  {
+    bf16_t* kr = dqkv + (rowbase + (kok ? mykey : 0)) * lddq + koff;
+    bf16_t* vr = dqkv + (rowbase + (kok ? mykey : 0)) * lddq + voff;
     const float vs = DROP ? dscale : 1.0f;
-#pragma unroll
-    for (int r = 0; r < 16; r += 4) {
-      const int d0 = acc_row(r, lane);
-      if (d0 < hd) {
-        uint2 w;
-        w.x = (uint32_t)f2bf(dk0[r] * kscale) | ((uint32_t)f2bf(dk0[r + 1] * kscale) << 16);
-        w.y = (uint32_t)f2bf(dk0[r + 2] * kscale) | ((uint32_t)f2bf(dk0[r + 3] * kscale) << 16);
-        *(uint2*)(kr + d0) = w;
-        w.x = (uint32_t)f2bf(dv0[r] * vs) | ((uint32_t)f2bf(dv0[r + 1] * vs) << 16);
-        w.y = (uint32_t)f2bf(dv0[r + 2] * vs) | ((uint32_t)f2bf(dv0[r + 3] * vs) << 16);
-        *(uint2*)(vr + d0) = w;
-      }
-      if (d0 + 32 < hd) {
-        uint2 w;
-        w.x = (uint32_t)f2bf(dk1[r] * kscale) | ((uint32_t)f2bf(dk1[r + 1] * kscale) << 16);
-        w.y = (uint32_t)f2bf(dk1[r + 2] * kscale) | ((uint32_t)f2bf(dk1[r + 3] * kscale) << 16);
-        *(uint2*)(kr + d0 + 32) = w;
-        w.x = (uint32_t)f2bf(dv1[r] * vs) | ((uint32_t)f2bf(dv1[r + 1] * vs) << 16);
-        w.y = (uint32_t)f2bf(dv1[r + 2] * vs) | ((uint32_t)f2bf(dv1[r + 3] * vs) << 16);
-        *(uint2*)(vr + d0 + 32) = w;
-      }
+    store_blk16(kr, dk0, kscale, kok, hd < 32 ? hd : 32, lane);
+    store_blk16(vr, dv0, vs, kok, hd < 32 ? hd : 32, lane);
+    if (hd > 32) {
+      store_blk16(kr + 32, dk1, kscale, kok, hd - 32, lane);
+      store_blk16(vr + 32, dv1, vs, kok, hd - 32, lane);
     }
   }
   if (bpart) {  // k / v bias gradient partials: column sums of this workgroup's dK, dV rows
