@@ -118,6 +118,11 @@ __device__ __forceinline__ float dpp_sum16(float t) {
 #ifndef CG_PERS_DIAG
 #define CG_PERS_DIAG 0
 #endif
+// timing-only diagnostic builds of the column-sum epilogue: 1 no DPP row sums, 2 no partial
+// stores (out-of-range offsets), 3 no accumulation
+#ifndef CG_COLSUM_DIAG
+#define CG_COLSUM_DIAG 0
+#endif
 #ifndef CG_PERS_L2HOT
 #define CG_PERS_L2HOT 0
 #endif
@@ -540,7 +545,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += r[j];
         }
-        if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
+        if constexpr ((EPI & CG_EPI_COLSUM) != 0 && CG_COLSUM_DIAG != 3) {
           const float keep = row < p.M ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) csum[c][j] = fmaf(keep, v[j], csum[c][j]);
@@ -556,17 +561,19 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
       // sum over the 16 row lanes sharing these columns, then lane r16 == 0 writes the wave's
       // 64-row partial (every lane issues the stores; the others at an out-of-range offset)
+      if (CG_COLSUM_DIAG != 1) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int c = 0; c < 2; ++c)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          csum[c][j] = dpp_sum16(csum[c][j]);
-        }
+          for (int j = 0; j < 8; ++j) {
+            csum[c][j] = dpp_sum16(csum[c][j]);
+          }
+      }
       const int prow = (m0 + wm) >> 6;
       const __amdgpu_buffer_rsrc_t rw = rsrc(p.ws, (long long)((p.M + 63) >> 6) * p.N * 4);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const uint32_t o = (r16 == 0 && col[c] < p.N) ? (uint32_t)(((long long)prow * p.N + col[c]) * 4) : OOR;
+        const uint32_t o = (CG_COLSUM_DIAG != 2 && r16 == 0 && col[c] < p.N) ? (uint32_t)(((long long)prow * p.N + col[c]) * 4) : OOR;
         bst(rw, o, (u32x4){__float_as_uint(csum[c][0]), __float_as_uint(csum[c][1]), __float_as_uint(csum[c][2]),
                            __float_as_uint(csum[c][3])});
         bst(rw, o + 16, (u32x4){__float_as_uint(csum[c][4]), __float_as_uint(csum[c][5]), __float_as_uint(csum[c][6]),

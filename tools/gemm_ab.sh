@@ -9,7 +9,7 @@ for r in $(seq 1 $rounds); do
   for lib in "$@"; do
     i=$((i+1))
     echo "== round $r lib $i $lib" >> $O/summary.txt
-    CG_LIB_PATH=$lib timeout -k 10 200 python tools/gemm_c4.py >> $O/summary.txt 2>&1 || exit 1
+    CG_LIB_PATH=$lib timeout -k 10 200 python tools/gemm_c4.py "${GEMM_ROWS:-}" >> $O/summary.txt 2>&1 || exit 1
   done
 done
 cat $O/summary.txt

@@ -96,7 +96,7 @@ def main():
             f0()
     torch.cuda.synchronize()
     best = {}
-    only = sys.argv[1] if len(sys.argv) > 1 else None  # e.g. "fc2 dX": time only matching rows
+    only = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] else None  # e.g. "fc2 dX": time only matching rows
     rows = [r for r in rows if only is None or r[0].startswith(only)]
     for _ in range(8):
         for name, _, _, f, f0 in rows:
