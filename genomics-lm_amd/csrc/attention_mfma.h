@@ -470,10 +470,10 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
         sx[r] = (j > kq || j < kl) ? -INFINITY : sx[r];
       }
     }
-    float ma = max3(sx[0], sx[1], sx[2]);
-#pragma unroll
-    for (int r = 3; r < 15; r += 2) ma = max3(ma, sx[r], sx[r + 1]);
-    const float mx = max_xhalf(max3(ma, sx[15], sx[15]));
+    // row max as a depth-3 tree of v_max3 (a linear chain was 8 dependent instructions)
+    const float ma = max3(max3(sx[0], sx[1], sx[2]), max3(sx[3], sx[4], sx[5]), max3(sx[6], sx[7], sx[8]));
+    const float mb = max3(max3(sx[9], sx[10], sx[11]), max3(sx[12], sx[13], sx[14]), sx[15]);
+    const float mx = max_xhalf(max3(ma, mb, mb));
     // NaN-safe: (-inf) - (-inf) compares false (a fully masked half never grows m)
     const bool grow = (mx - m) * c > 8.0f;
     if (__any(grow)) {
