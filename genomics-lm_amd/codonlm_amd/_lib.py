@@ -143,6 +143,7 @@ SIGNATURES = {
     "cg_attn_fwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp, vp]),
     "cg_attn_drop_mask_bytes": (sz, [i32, i32, i32]),
     "cg_attn_drop_mask": (i32, [i32, i32, i32, u32, f32, vp, vp]),
+    "cg_attn_fwd_keep": (i32, [i32, vp, i64, vp, vp, i64, vp, i32, i32, i32, i32, i32, i32, u32, f32, vp, vp]),
     "cg_attn_probs": (i32, [i32, vp, i64, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]),
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,

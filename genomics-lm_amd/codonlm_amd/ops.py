@@ -199,6 +199,20 @@ def attn_fwd(qkv, segstart, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, 
     return y, lse
 
 
+def attn_fwd_keep(qkv, segstart, B, T, H, KV, hd, drop_seed, drop_p, window=0, mask=None):
+    """Dropout forward that also writes the keep bits for the backward (cg_attn_fwd_keep): (y, lse, mask).
+    `mask` (optional): the cg_attn_drop_mask_bytes buffer to write into."""
+    if mask is None:
+        n = int(L.lib.cg_attn_drop_mask_bytes(B, T, H))
+        mask = torch.zeros(max(n, 4) // 4, dtype=torch.int32, device=qkv.device)
+    y = torch.empty(B * T, H * hd, dtype=qkv.dtype, device=qkv.device)
+    lse = torch.empty(B * H * T, dtype=torch.float32, device=qkv.device)
+    L.check(L.lib.cg_attn_fwd_keep(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
+                                   lse.data_ptr(), B, T, H, KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF,
+                                   float(drop_p), mask.data_ptr(), L.stream_ptr(qkv.device)), "cg_attn_fwd_keep")
+    return y, lse, mask
+
+
 def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None,
              bias_part=None):
     """dqkv; with bias_part (fp32 [B*ceil(T/128)][ld >= (H+2KV) hd], bf16 MFMA path) also the per-tile

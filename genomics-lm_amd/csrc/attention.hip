@@ -379,6 +379,24 @@ extern "C" int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const in
   return CG_OK;
 }
 
+extern "C" int cg_attn_fwd_keep(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, void* y,
+                                long long ldy, float* lse, int B, int T, int H, int KV, int hd, int window,
+                                uint32_t drop_seed, float drop_p, void* mask_out, void* stream) {
+  if (!(drop_p > 0.f) || drop_p >= 1.f || !mask_out) return CG_EINVAL;
+  if (KV <= 0 || H % KV) return CG_EINVAL;
+  if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
+  if (B == 0 || T == 0) return CG_OK;
+  if (dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, ldy))
+    return attn_fwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (bf16_t*)y, ldy, lse, B, T, H, KV, hd, window,
+                                drop_seed, cg_drop_threshold(drop_p), 1.f / (1.f - drop_p), 1.0f / sqrtf((float)hd),
+                                nullptr, (hipStream_t)stream, (uint32_t*)mask_out);
+  // other kernels: the words by the mask kernel, then the forward that reads them
+  const int rc = cg_attn_drop_mask(B, T, H, drop_seed, drop_p, mask_out, stream);
+  if (rc != CG_OK) return rc;
+  return cg_attn_fwd(dtype, qkv, ldqkv, segstart, y, ldy, lse, B, T, H, KV, hd, window, drop_seed, drop_p, mask_out,
+                     stream);
+}
+
 // delta (the vector path's rowsum(dO o O); the MFMA path's nd = -delta/dscale) | -lse2 (MFMA path)
 extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return 2 * (size_t)B * H * T * sizeof(float); }
 

@@ -233,6 +233,14 @@ __device__ __forceinline__ v8bf pack_b_keep(const v16f& x, int s, uint32_t w) {
   return __builtin_bit_cast(v8bf, v);
 }
 
+// keep bits applied to a packed B fragment from a word in "pair order": element pair r (r even)
+// of the lane at bit r/2 (even key) and r/2 + 16 (odd key) -- the forward's own hash words
+__device__ __forceinline__ v8bf keep_b_lin(v8bf u, int s, uint32_t w) {
+  v4u_a v = __builtin_bit_cast(v4u_a, u);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = keep_pk(v[i], w, 4 * s + i);
+  return __builtin_bit_cast(v8bf, v);
+}
 // keep bits applied to an already packed B fragment (rows 8s..8s+7 of an accumulator)
 __device__ __forceinline__ v8bf keep_b(v8bf u, int s, uint32_t w) {
   v4u_a v = __builtin_bit_cast(v4u_a, u);
@@ -400,14 +408,15 @@ __global__ __launch_bounds__(256) void attn_drop_mask_kernel(uint32_t* __restric
 // P, the row sum and the LSE; P <= 256 stays in range).
 // ============================================================================
 // DROP: 0 none, 1 keep bits hashed in the kernel, 2 keep bits read from attn_drop_mask_kernel's
-// query-major words
+// query-major words, 3 keep bits hashed in the kernel AND written in those words for the
+// backward (what attn_drop_mask_kernel would write for every (query, key) pair a query sees)
 template <int DROP, int HD>
 __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, long long ld,
                                                         const int32_t* __restrict__ seg, bf16_t* __restrict__ y,
                                                         long long ldy, float* __restrict__ lse, int T, int H, int KV,
                                                         int hd_rt, int window, uint32_t seed, uint32_t thr,
                                                         float dscale, float scale,
-                                                        const uint32_t* __restrict__ qmask, int wpr) {
+                                                        uint32_t* __restrict__ qmask, int wpr) {
   using namespace fa;
   constexpr int hd = HD;  // head dim is a compile-time constant: k-steps and the second
   (void)hd_rt;            // output block unroll without branches
@@ -438,8 +447,8 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
   const uint32_t tstride = (uint32_t)(KT * ld * 2);  // bytes per 64-row tile
   const float c = scale * 1.4426950408889634f;
   const uint32_t drow = (uint32_t)(((long long)b * H + hh) * T + myq);
-  const uint32_t hrow = DROP == 1 ? cg_row_hash(seed, drow) : 0u;
-  const uint32_t* qm = DROP == 2 ? qmask + ((long long)bh * T + (qok ? myq : 0)) * wpr : nullptr;
+  const uint32_t hrow = (DROP == 1 || DROP == 3) ? cg_row_hash(seed, drow) : 0u;
+  uint32_t* qm = (DROP == 2 || DROP == 3) ? qmask + ((long long)bh * T + (qok ? myq : 0)) * wpr : nullptr;
   constexpr int nks = (hd + 15) >> 4;
 
   float m = -INFINITY;
@@ -459,7 +468,8 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
   // and the P.V product of that half.  The tile's two S halves are issued back to back, so the
   // second half's QK^T MFMAs run while the first half is exponentiated, and the first half's
   // PV MFMAs while the second is (MFMA/VALU overlap inside one wave).
-  auto half = [&](v16f& sx, const int kb, const char* Vi, int k0, uint32_t wword, auto full_c)
+  // DROP == 3: the half's keep word in memory order, this lane's pairs only (wout)
+  auto half = [&](v16f& sx, const int kb, const char* Vi, int k0, uint32_t wword, uint32_t& wout, auto full_c)
                   __attribute__((always_inline)) {
     constexpr bool FULL = decltype(full_c)::value;
     if constexpr (!FULL) {
@@ -517,6 +527,26 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       pa = keep_b(pa, 0, w);
       pb = keep_b(pb, 1, w);
     }
+    if constexpr (DROP == 3) {
+      // the lane's 8 key pairs (pair r/2 of r = 0, 2, .., 14: colpair k0/2 + 16 kb + 2 hl +
+      // (r&3)/2 + 4 (r>>2)) hashed as attn_drop_mask_kernel does and shifted in, highest first, so
+      // pair r/2 lands on bit r/2 (even key) / 16 + r/2 (odd key)
+      const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl + 16u * (uint32_t)kb) * CG_COLK;
+      uint32_t ev = 0, od = 0;
+#pragma unroll
+      for (int r = 14; r >= 0; r -= 2) {
+        const uint32_t h = cg_pair_mix(hb + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2)) * CG_COLK);
+        ev = shift_in_keep<0>(ev, h, thr);
+        od = shift_in_keep<1>(od, h, thr);
+      }
+      const uint32_t wl = ev | (od << 16);
+      pa = keep_b_lin(pa, 0, wl);
+      pb = keep_b_lin(pb, 1, wl);
+      // memory ("pair-split") order: bit i of each half -> kbit(2i) = {0,1,4,5,8,9,12,13}[i], + 2 hl
+      const uint32_t sp = (wl & 0x00030003u) | ((wl & 0x000C000Cu) << 2) | ((wl & 0x00300030u) << 4) |
+                          ((wl & 0x00C000C0u) << 6);
+      wout = sp << (2 * hl);
+    }
     ATTN_SETPRIO(1);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 0), pa, o0, 0, 0, 0);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 0), pb, o0, 0, 0, 0);
@@ -542,9 +572,17 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
     // instructions, so each half's accumulator passes through a wait of 19 states first (>= the
     // 16-pass rule); without it v_max3 can read a stale accumulator and the row max varies run to run
     asm volatile("s_nop 15\n\ts_nop 2" : "+v"(s0));
-    half(s0, 0, Vi, k0, wc.x, full_c);
+    uint32_t w0 = 0, w1 = 0;
+    half(s0, 0, Vi, k0, wc.x, w0, full_c);
     asm volatile("s_nop 15\n\ts_nop 2" : "+v"(s1));
-    half(s1, 1, Vi, k0, wc.y, full_c);
+    half(s1, 1, Vi, k0, wc.y, w1, full_c);
+    if constexpr (DROP == 3) {
+      // the two lane halves hold the query's other pairs: or them, lane half 0 stores both words
+      const auto x0 = __builtin_amdgcn_permlane32_swap(w0, w0, false, false);
+      const auto x1 = __builtin_amdgcn_permlane32_swap(w1, w1, false, false);
+      if (qok && hl == 0)
+        *(uint2*)(qm + 2 * (k0 / KT)) = make_uint2(w0 | x0[0] | x0[1], w1 | x1[0] | x1[1]);
+    }
   };
   // the keep words are fetched one tile ahead (tiles above the wave's diagonal read words that
   // were never written; their pairs are causally masked)
@@ -1069,9 +1107,11 @@ static inline int attn_drop_mask_launch(uint32_t* mask, int B, int T, int H, uin
   return CG_OK;
 }
 
+// dmask_out (with thr): the keep words are made by the forward itself (DROP 3) instead of read
 static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, bf16_t* y, long long ldy,
                                        float* lse, int B, int T, int H, int KV, int hd, int window, uint32_t seed,
-                                       uint32_t thr, float dscale, float scale, const uint32_t* dmask, hipStream_t s) {
+                                       uint32_t thr, float dscale, float scale, const uint32_t* dmask, hipStream_t s,
+                                       uint32_t* dmask_out = nullptr) {
   dim3 g(B * H, cg_cdiv(T, 128));
   const size_t sh = 4 * fa::IMG;
   const int wpr = attn_drop_wpr(T);
@@ -1080,8 +1120,10 @@ static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_begin(CG_PROBE_ATTN_FWD, s);
 #define FWD(D, HDv)                                                                                          \
   hipLaunchKernelGGL((attn_fwd_mfma<D, HDv>), g, dim3(256), sh, s, qkv, ld, seg, y, ldy, lse, T, H, KV, hd, window, \
-                     seed, thr, dscale, scale, dmask, wpr)
-  if (thr && dmask) {
+                     seed, thr, dscale, scale, D == 3 ? dmask_out : const_cast<uint32_t*>(dmask), wpr)
+  if (thr && dmask_out) {
+    if (hd == 64) FWD(3, 64); else if (hd == 48) FWD(3, 48); else FWD(3, 32);
+  } else if (thr && dmask) {
     if (hd == 64) FWD(2, 64); else if (hd == 48) FWD(2, 48); else FWD(2, 32);
   } else if (thr) {
     if (hd == 64) FWD(1, 64); else if (hd == 48) FWD(1, 48); else FWD(1, 32);

@@ -36,15 +36,26 @@ template <> __device__ __forceinline__ void st_act<bf16_t>(bf16_t* p, float v) {
 // ---------------------------------------------------------------------------
 // wave / block reductions (64 lanes)
 // ---------------------------------------------------------------------------
+// All in VALU (no LDS round trip per step, as __shfl_xor's ds_bpermute would take): DPP within
+// each 16-lane row (quad xor 1, quad xor 2, row_half_mirror, row_mirror), then
+// v_permlane16_swap and v_permlane32_swap, whose two results called with (v, v) are the two
+// partners' values in every lane.  Every lane ends with the total, in a fixed order.
+template <typename F>
+__device__ __forceinline__ float wave_reduce(float v, F op) {
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false)));
+  v = op(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false)));
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = op(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  const auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return op(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  return wave_reduce(v, [](float a, float b) { return a + b; });
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  return wave_reduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 
 // ---------------------------------------------------------------------------

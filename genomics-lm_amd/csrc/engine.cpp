@@ -187,6 +187,10 @@ struct WS {
   }
 };
 
+static int g_fused_keep = [] {
+  const char* e = getenv("CG_ATTN_FUSED_KEEP");
+  return e ? atoi(e) : 1;
+}();
 struct LayerAct {
   float *mean1, *rstd1, *mean2, *rstd2, *lse, *xmid;
   void *h1, *qkv, *y, *h2, *a, *g, *gu, *s;
@@ -587,6 +591,48 @@ int defer_colsum(const Ctx& C, const void* dy, float* part, long long goff, int 
   return defer_reduce(C.m, part, C.D.d, np, C.D.d, G(C, goff), accumulate, C.s);
 }
 
+// d(head weight) (+)= alpha dlogits^T . xf  (M_out = Vp: pad rows of dlogits are zero; the hi
+// half of split-bf16 rows) as a split-K product of its own
+int head_dw_now(const Ctx& C, long long hoff, float alpha, int accumulate) {
+  const Acts& A = C.A;
+  cg_gemm_desc g = gdesc(C);
+  g.c_dtype = CG_F32;
+  g.M = C.D.Vp; g.N = C.D.d; g.K = (int)C.M;
+  g.A = A.dlogits; g.lda = A.ldl; g.a_kcontig = 0;
+  g.B = A.xf; g.ldb = C.D.d; g.b_kcontig = 0;
+  g.C = G(C, hoff); g.ldc = C.D.d;
+  g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
+  g.alpha = alpha;
+  g.split_k = pick_split(C, C.D.Vp, C.D.d, C.M);
+  g.workspace = A.splitws;
+  g.ws_bytes = A.nb.splitws;
+  return cg_gemm(&g, C.s);
+}
+// The tied head's weight gradient, deferred from phase 0 into the first dW group's grouped
+// launch (bf16, no aux heads): a few more tiles beside the group's (the C4 remainder group fills
+// 192 of 256 CUs) instead of a split-K product (22 us) and its slab reduction (7 us).  Its
+// operands (dlogits, xf) are not written again before that launch, and the tied gradient
+// (tok_emb) is final only after phase 2, so no data-parallel bucket sees it early.  Keyed by
+// model like the pending reductions; phase 0 (re)sets it, phase 2 runs it if no group did.
+struct HeadDw {
+  const cg_model* m;
+  long long hoff;
+  float alpha;
+  int accumulate;
+  bool on;
+};
+HeadDw& head_dw_pending(const cg_model* m) {
+  static std::vector<HeadDw> v;
+  for (auto& e : v)
+    if (e.m == m) return e;
+  v.push_back(HeadDw{m, 0, 1.0f, 0, false});
+  return v.back();
+}
+static int g_head_dw_defer = [] {
+  const char* e = getenv("CG_HEAD_DW_DEFER");
+  return e ? atoi(e) : 1;
+}();
+
 // The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
 // bf16 mode (gemm_dw.h), the per-product GEMMs in fp32 parity mode.
 int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
@@ -619,6 +665,16 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
     }
     CK(add(sl.gattn, d, a.y, d, o.wp));
     CK(add(sl.dqkv, D.Nqkv, a.h1, d, o.wqkv));
+  }
+  HeadDw& hd = head_dw_pending(C.m);
+  if (hd.on && C.dt == CG_BF16 && grp.n < CG_DW_MAX) {
+    cg_dw_product& q = grp.p[grp.n++];
+    q.A = C.A.dlogits; q.lda = C.A.ldl;
+    q.B = C.A.xf; q.ldb = d;
+    q.C = G(C, hd.hoff); q.ldc = d;
+    q.N_out = D.Vp; q.K_out = d;
+    q.alpha = hd.alpha; q.accumulate = hd.accumulate;
+    hd.on = false;
   }
   if (C.dt == CG_BF16 && grp.n) return cg_gemm_dw_grouped(&grp, C.s);
   return CG_OK;
@@ -846,7 +902,9 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   const float eps = m->cfg.ln_eps > 0 ? m->cfg.ln_eps : 1e-5f;
   m->logits = logits ? logits : A.logits_int;
 
-  const bool masks = p > 0.f && D.L > 0 && A.la[0].dmask;
+  // the keep bits: made by each block's attention forward itself (default), or by the mask kernel
+  // on a side stream ahead of the forward (CG_ATTN_FUSED_KEEP=0)
+  const bool masks = p > 0.f && D.L > 0 && A.la[0].dmask && !g_fused_keep;
   MaskStream* ms = masks ? mask_stream(D.L) : nullptr;
   if (ms) {
     if (hipEventRecord(ms->start, C.s) != hipSuccess || hipStreamWaitEvent(ms->s, ms->start, 0) != hipSuccess)
@@ -870,13 +928,18 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     CK(cg_gemm(&g, C.s));
     if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
     const void* dmask = p > 0.f ? a.dmask : nullptr;
-    if (dmask && ms) {
-      if (hipStreamWaitEvent(C.s, ms->done[l], 0) != hipSuccess) return CG_ELAUNCH;
-    } else if (dmask) {
-      CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+    if (dmask && g_fused_keep) {
+      CK(cg_attn_fwd_keep(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV,
+                          D.hd, window, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+    } else {
+      if (dmask && ms) {
+        if (hipStreamWaitEvent(C.s, ms->done[l], 0) != hipSuccess) return CG_ELAUNCH;
+      } else if (dmask) {
+        CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+      }
+      CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
+                     window, site_seed(seed, l, SITE_ATTN), p, dmask, C.s));
     }
-    CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
-                   window, site_seed(seed, l, SITE_ATTN), p, dmask, C.s));
     g = lin_fwd(C, a.y, d, o.wp, d, d, d, a.xmid, d);
     g.c_dtype = CG_F32;
     g.epilogue = CG_EPI_BIAS | CG_EPI_RESID; g.bias = P(C, o.bp); g.resid = xl; g.ldr = d;
@@ -986,24 +1049,18 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (m->targets && m->head_grad_scale_dev)  // d(objective)/d(loss) still on the device
       CK(cg_scale_dev(C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, (int)M, D.Vp, m->head_grad_scale_dev,
                       C.s));
+    HeadDw& hd = head_dw_pending(m);
+    hd.on = false;
     if (m->targets) {
-      // d(head weight) = s dlogits^T . xf     (M_out = Vp: pad rows of dlogits are zero; the hi
-      // half of split-bf16 rows)
-      cg_gemm_desc g = gdesc(C);
-      g.c_dtype = CG_F32;
-      g.M = D.Vp; g.N = d; g.K = (int)M;
-      g.A = A.dlogits; g.lda = A.ldl; g.a_kcontig = 0;
-      g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
-      g.C = G(C, hoff); g.ldc = d;
-      g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
-      g.alpha = m->head_grad_scale;
-      g.split_k = pick_split(C, D.Vp, d, M);
-      g.workspace = A.splitws;
-    g.ws_bytes = A.nb.splitws;
-      g.ws_bytes = A.nb.splitws;
-      CK(cg_gemm(&g, C.s));
+      // d(head weight) = s dlogits^T . xf: deferred into the first dW group when nothing else
+      // adds into it before that launch (the aux heads do, and reuse dlogits)
+      if (g_head_dw_defer && C.dt == CG_BF16 && D.L > 0 && m->cfg.tie_embeddings && !m->cfg.termination_aux &&
+          m->cfg.n_offsets <= 0)
+        hd = HeadDw{m, hoff, m->head_grad_scale, accumulate, true};
+      else
+        CK(head_dw_now(C, hoff, m->head_grad_scale, accumulate));
       // dxf = s dlogits . E
-      g = head_dx(C, hoff, A.dtmp, d);
+      cg_gemm_desc g = head_dx(C, hoff, A.dtmp, d);
       g.c_dtype = CG_F32;
       g.alpha = m->head_grad_scale;
       CK(cg_gemm(&g, C.s));
@@ -1106,6 +1163,11 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   }
   if (phase == 2) {
     CK(flush_reduce(m, C.s));  // nothing is pending after block 0; kept for partial phase sequences
+    HeadDw& hd = head_dw_pending(m);
+    if (hd.on) {  // a partial phase sequence: no dW group took the head's product
+      hd.on = false;
+      CK(head_dw_now(C, hd.hoff, hd.alpha, hd.accumulate));
+    }
     // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
     const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
     CK(cg_embed_bwd(m->idx, A.g, G(C, C.Lo.tok), nullptr, C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,

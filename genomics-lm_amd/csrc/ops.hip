@@ -648,10 +648,12 @@ extern "C" int cg_embed_fwd(const int64_t* idx, const float* tok_emb, const floa
   return CG_OK;
 }
 
-constexpr int EMB_RCHUNKS = 32;
+constexpr int EMB_RCHUNKS = 32;   // row chunks of embed_bwd_tok_kernel (64 columns per workgroup)
+constexpr int EMB_RCHUNKS2 = 64;  // row chunks of embed_bwd_tok2_kernel (128 columns per workgroup)
+constexpr int EMB_V2 = 80;        // largest vocabulary of the latter (4 [V][128] fp32 slabs in LDS)
 extern "C" size_t cg_embed_bwd_workspace(int B, int T, int V, int d) {
   (void)B; (void)T;
-  return (size_t)EMB_RCHUNKS * V * d * sizeof(float);
+  return (size_t)(V <= EMB_V2 ? EMB_RCHUNKS2 : EMB_RCHUNKS) * V * d * sizeof(float);
 }
 
 // per (64-column chunk, row chunk): each wave accumulates its own rows into its own LDS
@@ -700,6 +702,58 @@ __global__ __launch_bounds__(256) void embed_bwd_tok_kernel(const int64_t* __res
   }
 }
 
+// V <= EMB_V2: each lane owns two adjacent columns (one float2 load and one keep hash per row:
+// the pair is the hash's column pair), a wave spans 128 columns and keeps 16 rows' loads in
+// flight -- 4x the bytes in flight of the kernel above, whose 4-byte lanes left the C4 pass
+// latency-bound (24 us for 34 MB).  Same fixed order: rows of a wave in order, slabs 0..3, chunks.
+__global__ __launch_bounds__(256) void embed_bwd_tok2_kernel(const int64_t* __restrict__ idx, const float* __restrict__ g,
+                                                             float* __restrict__ part, int rows, int V, int d,
+                                                             uint32_t seed, uint32_t thr, float dscale) {
+  extern __shared__ __attribute__((aligned(16))) float acc[];  // [4][V][128]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 128 + 2 * lane;
+  for (int e = threadIdx.x; e < V * 128; e += 256) *(float4*)(acc + 4 * e) = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float* mine = acc + wave * V * 128 + 2 * lane;
+  auto add = [&](int r, int tk, float2 v) {
+    if (thr) {
+      const uint32_t h = cg_hash_pair(seed, (uint32_t)r, (uint32_t)c >> 1);
+      v.x = (h & 0xFFFFu) >= thr ? v.x * dscale : 0.f;
+      v.y = (h >> 16) >= thr ? v.y * dscale : 0.f;
+    }
+    float2* a = (float2*)(mine + tk * 128);
+    float2 t = *a;
+    t.x += v.x;
+    t.y += v.y;
+    *a = t;
+  };
+  if (c < d) {
+    int r = r0 + wave;
+    for (; r + 60 < r1; r += 64) {  // 16 rows' loads in flight, added in row order
+      int tk[16];
+      float2 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        tk[u] = (int)idx[r + 4 * u];
+        v[u] = *(const float2*)(g + (long long)(r + 4 * u) * d + c);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) add(r + 4 * u, tk[u], v[u]);
+    }
+    for (; r < r1; r += 4) add(r, (int)idx[r], *(const float2*)(g + (long long)r * d + c));
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < V * 128; e += 256) {
+    const int v = e >> 7, l = e & 127, cc = blockIdx.x * 128 + l;
+    if (cc < d) {
+      const float sm = acc[e] + acc[V * 128 + e] + acc[2 * V * 128 + e] + acc[3 * V * 128 + e];
+      part[((long long)blockIdx.y * V + v) * d + cc] = sm;
+    }
+  }
+}
+
 __global__ void embed_bwd_tok_reduce(const float* __restrict__ part, float* __restrict__ dtok, int nch, int V, int d,
                                      int accumulate) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -735,7 +789,25 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, flo
   hipStream_t s = (hipStream_t)stream;
   const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-  if (dtok) {
+  static const int emb2 = [] {
+    const char* e = getenv("CG_EMB_TOK2");  // 0: the 64-column kernel (A/B switch)
+    return e ? atoi(e) : 1;
+  }();
+  if (dtok && emb2 && V <= EMB_V2 && d % 2 == 0 && ((uintptr_t)g & 7) == 0) {
+    const int nch = EMB_RCHUNKS2 > rows ? rows : EMB_RCHUNKS2;
+    const size_t sh = (size_t)4 * V * 128 * sizeof(float);
+    static bool attr2 = false;
+    if (!attr2) {
+      (void)hipFuncSetAttribute((const void*)embed_bwd_tok2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      attr2 = true;
+    }
+    hipLaunchKernelGGL(embed_bwd_tok2_kernel, dim3(cg_cdiv(d, 128), nch), dim3(256), sh, s, idx, g, (float*)ws, rows,
+                       V, d, drop_seed, thr, dscale);
+    CG_LAUNCH_CHECK();
+    hipLaunchKernelGGL(embed_bwd_tok_reduce, dim3(cg_cdiv(V * d, 256)), dim3(256), 0, s, (const float*)ws, dtok,
+                       nch, V, d, accumulate);
+    CG_LAUNCH_CHECK();
+  } else if (dtok) {
     int nch = EMB_RCHUNKS;
     if (nch > rows) nch = rows;
     const size_t sh = (size_t)4 * V * 64 * sizeof(float);
@@ -1210,12 +1282,24 @@ extern "C" int cg_colsum(int dtype, const void* X, long long ldx, int rows, int 
 // model_tiny_gpt.py:343-349). L = sum_valid[(1-e) w_y nll_y + e/V sum_c w_c nll_c] / sum_valid w_y
 // ===========================================================================
 constexpr int CE_BLK = 4096;  // rows per block = 4 waves x 1 row, grid-strided beyond 16384 rows
-// sum_valid w_y: 1024 threads, 4 independent load chains each, fixed-order tree
+// sum_valid w_y: 1024 threads, 4 independent sums each, fixed-order tree.  16 rows per thread and
+// round: all 16 targets are loaded before any class-weight gather (two load latencies per round
+// instead of eight dependent pairs: C4's 16384 rows took 10.5 us in 4-row rounds)
 __global__ __launch_bounds__(1024) void ce_denom_kernel(const int64_t* __restrict__ tg, int rows, const float* __restrict__ w,
                                                         int ignore, float* __restrict__ ws) {
   __shared__ float red[1024];
   float s4[4] = {0.f, 0.f, 0.f, 0.f};
   int r = threadIdx.x;
+  for (; r + 15 * 1024 < rows; r += 16 * 1024) {
+    int64_t t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) t[u] = tg[r + 1024 * u];
+    float wt[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) wt[u] = t[u] == ignore ? 0.f : (w ? w[t[u]] : 1.0f);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s4[u & 3] += wt[u];
+  }
   for (; r + 3072 < rows; r += 4096)
 #pragma unroll
     for (int u = 0; u < 4; ++u) {

@@ -199,6 +199,15 @@ int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
  * same seed and p, or NULL to hash in the kernels (identical keep decisions). */
 size_t cg_attn_drop_mask_bytes(int B, int T, int H);
 int cg_attn_drop_mask(int B, int T, int H, uint32_t drop_seed, float drop_p, void* mask, void* stream);
+/* cg_attn_fwd with dropout (0 < drop_p < 1) whose forward also writes the keep bits into mask_out
+ * (a cg_attn_drop_mask_bytes buffer) for the backward: the bf16 MFMA forward hashes the keep
+ * decisions itself and stores, for every (query, key) pair a query can see, the bits
+ * cg_attn_drop_mask would store (bits of pairs no query sees are left as they are); other paths
+ * run cg_attn_drop_mask and then cg_attn_fwd.  Replaces the drop_mask + fwd pair of
+ * model_tiny_gpt.py:104-114 (SDPA dropout_p) in the training forward. */
+int cg_attn_fwd_keep(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, void* y,
+                     long long ldy, float* lse, int B, int T, int H, int KV, int hd, int window,
+                     uint32_t drop_seed, float drop_p, void* mask_out, void* stream);
 /* Attention probabilities materialised (the manual path's `last_attn`, model_tiny_gpt.py:117-128):
  * out fp32 [B][H][T][T] = exp(S/sqrt(hd) - lse) on visible (query, key), 0 elsewhere, from the
  * forward's qkv rows (post-RoPE) and lse.  Inspection path. */

@@ -466,6 +466,47 @@ def test_attention_drop_mask_path_matches_hash_path(B, T, H, KV, hd):
     assert float((d1 - d0).norm() / d0.norm()) <= 1e-3
 
 
+@pytest.mark.parametrize("B,T,H,KV,hd,window,sep", [(2, 1024, 8, 8, 64, 0, True), (2, 512, 8, 4, 48, 0, True),
+                                                    (1, 200, 4, 2, 32, 0, False), (1, 129, 2, 1, 64, 0, True),
+                                                    (1, 300, 2, 2, 64, 70, False)])
+def test_attention_fused_keep_forward(B, T, H, KV, hd, window, sep):
+    """cg_attn_fwd_keep: the forward that hashes its own keep decisions writes, for every (query, key)
+    pair a query sees, exactly attn_drop_mask's bit, and its y / lse equal the forward that reads
+    attn_drop_mask's words (bitwise); the backward reading the fused words equals the one reading
+    the mask kernel's."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(7 * hd + T)
+    N = (H + 2 * KV) * hd
+    qkv = _bf(torch.randn(B * T, N, generator=g)).to(DEV, torch.bfloat16)
+    idx = torch.randint(4, 68, (B, T), generator=g)
+    if sep:
+        idx[0, T // 3] = 3
+        idx[-1, (2 * T) // 3] = 3
+    seg = ops.segment_starts(idx.to(DEV), 3 if sep else -1)
+    seed, p = 2024, 0.1
+    ref = ops.attn_drop_mask(B, T, H, seed, p, DEV)
+    y0, l0 = ops.attn_fwd(qkv, seg, B, T, H, KV, hd, window=window, drop_seed=seed, drop_p=p, drop_mask=ref)
+    y1, l1, mk = ops.attn_fwd_keep(qkv, seg, B, T, H, KV, hd, seed, p, window=window)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1) and torch.equal(l0, l1)
+    wpr = 2 * ((T + 63) // 64)
+    a = _mask_bits(ref.view(B * H, T, wpr), T)
+    b = _mask_bits(mk.view(B * H, T, wpr), T)
+    # visible pairs: causal, same SEP segment (key >= segment start), inside the window
+    q = np.arange(T)[:, None]
+    k = np.arange(T)[None, :]
+    st = seg.view(B, T).cpu().numpy().astype(np.int64)
+    vis = (k <= q)[None] & (k >= st[:, :, None])
+    if window:
+        vis = vis & (k > q - window)[None]
+    vis = np.repeat(vis, H, axis=0).reshape(B * H, T, T)
+    assert np.array_equal(a & vis, b & vis)
+    dy = _bf(torch.randn(B * T, H * hd, generator=g)).to(DEV, torch.bfloat16)
+    d0 = ops.attn_bwd(qkv, seg, y0, dy, l0, B, T, H, KV, hd, window=window, drop_seed=seed, drop_p=p, drop_mask=ref)
+    d1 = ops.attn_bwd(qkv, seg, y1, dy, l1, B, T, H, KV, hd, window=window, drop_seed=seed, drop_p=p, drop_mask=mk)
+    assert torch.equal(d0, d1)
+
+
 @pytest.mark.parametrize("eps,weighted", [(0.0, False), (0.05, False), (0.1, True)])
 def test_cross_entropy(eps, weighted):
     ops = _ops()
