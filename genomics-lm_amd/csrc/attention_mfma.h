@@ -233,14 +233,6 @@ __device__ __forceinline__ v8bf pack_b_keep(const v16f& x, int s, uint32_t w) {
   return __builtin_bit_cast(v8bf, v);
 }
 
-// keep bits applied to a packed B fragment from a word in "pair order": element pair r (r even)
-// of the lane at bit r/2 (even key) and r/2 + 16 (odd key) -- the forward's own hash words
-__device__ __forceinline__ v8bf keep_b_lin(v8bf u, int s, uint32_t w) {
-  v4u_a v = __builtin_bit_cast(v4u_a, u);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = keep_pk(v[i], w, 4 * s + i);
-  return __builtin_bit_cast(v8bf, v);
-}
 // keep bits applied to an already packed B fragment (rows 8s..8s+7 of an accumulator)
 __device__ __forceinline__ v8bf keep_b(v8bf u, int s, uint32_t w) {
   v4u_a v = __builtin_bit_cast(v4u_a, u);
@@ -448,6 +440,8 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
   const float c = scale * 1.4426950408889634f;
   const uint32_t drow = (uint32_t)(((long long)b * H + hh) * T + myq);
   const uint32_t hrow = (DROP == 1 || DROP == 3) ? cg_row_hash(seed, drow) : 0u;
+  // DROP == 3: thr - 1 in both 16-bit halves (1 <= thr <= 65536 on this path)
+  const uint32_t thr2m1 = (thr - 1u) | ((thr - 1u) << 16);
   uint32_t* qm = (DROP == 2 || DROP == 3) ? qmask + ((long long)bh * T + (qok ? myq : 0)) * wpr : nullptr;
   constexpr int nks = (hd + 15) >> 4;
 
@@ -532,16 +526,22 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       // (r&3)/2 + 4 (r>>2)) hashed as attn_drop_mask_kernel does and shifted in, highest first, so
       // pair r/2 lands on bit r/2 (even key) / 16 + r/2 (odd key)
       const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl + 16u * (uint32_t)kb) * CG_COLK;
-      uint32_t ev = 0, od = 0;
+      v4u_a va = __builtin_bit_cast(v4u_a, pa), vb = __builtin_bit_cast(v4u_a, pb);
+      uint32_t wl = 0;
 #pragma unroll
       for (int r = 14; r >= 0; r -= 2) {
         const uint32_t h = cg_pair_mix(hb + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2)) * CG_COLK);
-        ev = shift_in_keep<0>(ev, h, thr);
-        od = shift_in_keep<1>(od, h, thr);
+        // both halves at once: keep = 1 where half >= thr (clamped h - (thr - 1) > 0), shifted into
+        // wl, and the packed pair's 16-bit lanes and-ed with 0 - keep
+        uint32_t kp;
+        asm("v_pk_sub_u16 %0, %2, %3 clamp\n\tv_pk_min_u16 %0, %0, 1 op_sel_hi:[1,0]\n\t"
+            "v_lshl_or_b32 %1, %1, 1, %0\n\tv_pk_sub_u16 %0, 0, %0"
+            : "=&v"(kp), "+v"(wl) : "v"(h), "s"(thr2m1));
+        if (r < 8) va[r >> 1] &= kp;
+        else vb[(r - 8) >> 1] &= kp;
       }
-      const uint32_t wl = ev | (od << 16);
-      pa = keep_b_lin(pa, 0, wl);
-      pb = keep_b_lin(pb, 1, wl);
+      pa = __builtin_bit_cast(v8bf, va);
+      pb = __builtin_bit_cast(v8bf, vb);
       // memory ("pair-split") order: bit i of each half -> kbit(2i) = {0,1,4,5,8,9,12,13}[i], + 2 hl
       const uint32_t sp = (wl & 0x00030003u) | ((wl & 0x000C000Cu) << 2) | ((wl & 0x00300030u) << 4) |
                           ((wl & 0x00C000C0u) << 6);
