@@ -1,5 +1,6 @@
 """One forward + backward of the C4 attention (dropout 0.1, SEP segments), for PMC passes.
-Uses the engine's path: keep bits precomputed by cg_attn_drop_mask (ATTN_HASH=1: in-kernel hash)."""
+Uses the engine's path: keep bits written by the forward (cg_attn_fwd_keep); ATTN_MASK=1: made by
+cg_attn_drop_mask first (the round-2 path), ATTN_HASH=1: hashed in every kernel."""
 import os
 import sys
 from pathlib import Path
@@ -13,9 +14,13 @@ qkv = (torch.randn(B * T, 3 * H * hd, generator=g) * 0.5).to("cuda", torch.bfloa
 idx = torch.randint(4, 68, (B, T), generator=g)
 seg = ops.segment_starts(idx.to("cuda"), 3)
 hashed = os.environ.get("ATTN_HASH") == "1"
+separate = os.environ.get("ATTN_MASK") == "1"
 for _ in range(2):
-    mask = None if hashed else ops.attn_drop_mask(B, T, H, 5, 0.1, "cuda")
-    y, lse = ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask)
+    if hashed or separate:
+        mask = None if hashed else ops.attn_drop_mask(B, T, H, 5, 0.1, "cuda")
+        y, lse = ops.attn_fwd(qkv, seg, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask)
+    else:
+        y, lse, mask = ops.attn_fwd_keep(qkv, seg, B, T, H, H, hd, 5, 0.1)
     dy = torch.randn_like(y)
     ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask)
 torch.cuda.synchronize()
