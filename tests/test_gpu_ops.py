@@ -507,6 +507,34 @@ def test_attention_fused_keep_forward(B, T, H, KV, hd, window, sep):
     assert torch.equal(d0, d1)
 
 
+@pytest.mark.parametrize("V,d,p,acc", [(68, 512, 0.1, 0), (68, 256, 0.0, 1), (80, 384, 0.1, 0), (150, 256, 0.1, 1),
+                                    (150, 128, 0.0, 0)])
+def test_embed_bwd_token_rows(V, d, p, acc):
+    """cg_embed_bwd's token-embedding gradient -- the float2 kernel (V <= 80) and the 64-column one --
+    against an fp64 index_add of the dropout-kept rows (the oracle's keep hash), plain and accumulating."""
+    from codonlm_amd import _lib as L
+    B, T = 3, 217  # ragged: 651 rows, not a multiple of either kernel's row chunking
+    M = B * T
+    g = torch.Generator().manual_seed(V + d)
+    idx = torch.randint(0, V, (B, T), generator=g)
+    idx[0, :40] = 5  # one token on many consecutive rows (the serial per-lane add chain)
+    gr = torch.randn(M, d, generator=g)
+    seed = 77
+    keep = O.dropout_keep(seed, np.arange(M)[:, None], np.arange(d)[None, :], p) if p > 0 else np.ones((M, d), bool)
+    scale = 1.0 / (1.0 - p) if p > 0 else 1.0
+    base = torch.randn(V, d, generator=g)
+    ref = (base.double() if acc else torch.zeros(V, d, dtype=torch.float64)).index_add_(
+        0, idx.view(-1), gr.double() * torch.from_numpy(keep).double() * scale)
+    idx_d, gr_d = idx.to(DEV), gr.to(DEV)
+    dtok = base.to(DEV) if acc else torch.full((V, d), float("nan"), device=DEV)
+    need = int(L.lib.cg_embed_bwd_workspace(B, T, V, d))
+    ws = torch.empty(need // 4 + 1, dtype=torch.float32, device=DEV)
+    assert L.lib.cg_embed_bwd(idx_d.data_ptr(), gr_d.data_ptr(), dtok.data_ptr(), None, B, T, V, d, seed, p, acc,
+                              ws.data_ptr(), need, L.stream_ptr(DEV)) == 0
+    torch.cuda.synchronize()
+    assert torch.allclose(dtok.cpu().double(), ref, atol=2e-4, rtol=1e-5)
+
+
 @pytest.mark.parametrize("eps,weighted", [(0.0, False), (0.05, False), (0.1, True)])
 def test_cross_entropy(eps, weighted):
     ops = _ops()
