@@ -191,10 +191,20 @@ extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, co
 }
 
 extern "C" int cg_layernorm_bwd_blocks(int rows) {
-  // 16 rows per block (4 per wave), at most 1024 blocks: measured faster than 32 rows/block
-  // (C4: 29.7 vs 38.2 us) although the dgamma/dbeta partial reduction then reads 2x more
-  int b = cg_cdiv(rows, 16);
-  return b > 1024 ? 1024 : (b < 1 ? 1 : b);
+  // 32 rows per block (8 per wave), at most 1024 blocks.  Round 2 measured 16 rows faster (C4:
+  // 29.7 vs 38.2 us); with the round-2/3 kernel the two run alike (24.1 vs 24.5 us) and 32 halves
+  // the partial rows the deferred column reduction reads (18.9 -> 14.9 us per group): C4 step
+  // -23..-46 us (3 interleaved same-box runs).  CG_LN_BWD_ROWS / CG_LN_BWD_MAXBLK: A/B switches.
+  static const int rpb = [] {
+    const char* e = getenv("CG_LN_BWD_ROWS");
+    return e && atoi(e) > 0 ? atoi(e) : 32;
+  }();
+  static const int maxb = [] {
+    const char* e = getenv("CG_LN_BWD_MAXBLK");
+    return e && atoi(e) > 0 ? atoi(e) : 1024;
+  }();
+  int b = cg_cdiv(rows, rpb);
+  return b > maxb ? maxb : (b < 1 ? 1 : b);
 }
 extern "C" size_t cg_layernorm_bwd_workspace(int rows, int cols, int want_col) {
   return (size_t)cg_layernorm_bwd_blocks(rows) * (size_t)(want_col ? 3 : 2) * (size_t)(cols > 0 ? cols : 0) * sizeof(float);
