@@ -774,6 +774,39 @@ __global__ void embed_bwd_tok_reduce(const float* __restrict__ part, float* __re
   dtok[e] = accumulate ? dtok[e] + s : s;
 }
 
+// d % 4 == 0: each thread sums 4 adjacent columns (one float4 per batch row, the B rows' loads
+// independent), per element in the same b order as the scalar kernel
+__global__ void embed_bwd_pos4_kernel(const float* __restrict__ g, float* __restrict__ dpos, int B, int T, int d,
+                                      uint32_t seed, uint32_t thr, float dscale, int accumulate) {
+  const long long e4 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (e4 * 4 >= (long long)T * d) return;
+  const long long e = e4 * 4;
+  const int t = (int)(e / d), c = (int)(e % d);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b = 0; b < B; ++b) {
+    const long long m = (long long)b * T + t;
+    float4 v = *(const float4*)(g + m * d + c);
+    if (thr) {
+      const uint32_t h0 = cg_hash_pair(seed, (uint32_t)m, (uint32_t)c >> 1);
+      const uint32_t h1 = cg_hash_pair(seed, (uint32_t)m, ((uint32_t)c >> 1) + 1u);
+      v.x = (h0 & 0xFFFFu) >= thr ? v.x * dscale : 0.f;
+      v.y = (h0 >> 16) >= thr ? v.y * dscale : 0.f;
+      v.z = (h1 & 0xFFFFu) >= thr ? v.z * dscale : 0.f;
+      v.w = (h1 >> 16) >= thr ? v.w * dscale : 0.f;
+    }
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  float4* o = (float4*)(dpos + e);
+  if (accumulate) {
+    const float4 a = *o;
+    s = make_float4(a.x + s.x, a.y + s.y, a.z + s.z, a.w + s.w);
+  }
+  *o = s;
+}
+
 __global__ void embed_bwd_pos_kernel(const float* __restrict__ g, float* __restrict__ dpos, int B, int T, int d,
                                      uint32_t seed, uint32_t thr, float dscale, int accumulate) {
   const long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -835,7 +868,11 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, flo
     CG_LAUNCH_CHECK();
   }
   if (dpos) {
-    hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(cg_cdiv((long long)T * d, 256)), dim3(256), 0, s, g, dpos, B, T,
+    if (d % 4 == 0 && ((uintptr_t)g & 15) == 0 && ((uintptr_t)dpos & 15) == 0)
+      hipLaunchKernelGGL(embed_bwd_pos4_kernel, dim3(cg_cdiv((long long)T * d / 4, 256)), dim3(256), 0, s, g, dpos, B,
+                         T, d, drop_seed, thr, dscale, accumulate);
+    else
+      hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3(cg_cdiv((long long)T * d, 256)), dim3(256), 0, s, g, dpos, B, T,
                        d, drop_seed, thr, dscale, accumulate);
     CG_LAUNCH_CHECK();
   }

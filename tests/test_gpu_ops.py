@@ -533,6 +533,15 @@ def test_embed_bwd_token_rows(V, d, p, acc):
                               ws.data_ptr(), need, L.stream_ptr(DEV)) == 0
     torch.cuda.synchronize()
     assert torch.allclose(dtok.cpu().double(), ref, atol=2e-4, rtol=1e-5)
+    # the position rows: sum over the batch of the same kept rows (float4 kernel when d % 4 == 0)
+    pbase = torch.randn(T, d, generator=g)
+    kept = gr.double() * torch.from_numpy(keep).double() * scale
+    pref = kept.view(B, T, d).sum(0) + (pbase.double() if acc else 0.0)
+    dpos = pbase.to(DEV) if acc else torch.full((T, d), float("nan"), device=DEV)
+    assert L.lib.cg_embed_bwd(idx_d.data_ptr(), gr_d.data_ptr(), None, dpos.data_ptr(), B, T, V, d, seed, p, acc,
+                              None, 0, L.stream_ptr(DEV)) == 0
+    torch.cuda.synchronize()
+    assert torch.allclose(dpos.cpu().double(), pref, atol=2e-5, rtol=1e-5)
 
 
 @pytest.mark.parametrize("eps,weighted", [(0.0, False), (0.05, False), (0.1, True)])
