@@ -342,7 +342,8 @@ __device__ __forceinline__ int lo_of(const int32_t* seg, long long rowbase, int 
 // ============================================================================
 // attention-dropout keep bits, precomputed once per layer: keep = cg_keep(seed, (b*H+h)*T + q,
 // key, thr) exactly, so the attention kernels test one bit per (query, key) instead of hashing
-//   qmask[(bh*T + q)*wpr + w]: keys 32w..32w+31 of query q
+//   qmask[((bh*nt + t)*T + q)*2 + w]: keys 64t + 32w .. +31 of query q (nt = ceil(T/64) key tiles;
+//   tile-major, so the 32 queries of a wave read / write 256 contiguous bytes per tile)
 // in "pair-split" order (bit c = key 2c, bit 16 + c = key 2c + 1: fa::kbit), which lets the
 // forward apply two bits to a packed bf16 pair at once.  wpr = 2*ceil(T/64) (every 64-key tile
 // has both of its words in bounds).  One wave per 64x64 block of the causal lower triangle,
@@ -388,7 +389,7 @@ __global__ __launch_bounds__(256) void attn_drop_mask_kernel(uint32_t* __restric
     }
     wq[w] = ev | (od << 16);
   }
-  *(uint2*)(qmask + (bh * T + q) * wpr + 2 * kb) = make_uint2(wq[0], wq[1]);
+  *(uint2*)(qmask + ((bh * (wpr >> 1) + kb) * T + q) * 2) = make_uint2(wq[0], wq[1]);
 }
 
 // ============================================================================
@@ -442,7 +443,8 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
   const uint32_t hrow = (DROP == 1 || DROP == 3) ? cg_row_hash(seed, drow) : 0u;
   // DROP == 3: thr - 1 in both 16-bit halves (1 <= thr <= 65536 on this path)
   const uint32_t thr2m1 = (thr - 1u) | ((thr - 1u) << 16);
-  uint32_t* qm = (DROP == 2 || DROP == 3) ? qmask + ((long long)bh * T + (qok ? myq : 0)) * wpr : nullptr;
+  uint32_t* qm = (DROP == 2 || DROP == 3) ? qmask + ((long long)bh * (wpr >> 1) * T + (qok ? myq : 0)) * 2 : nullptr;
+  const long long tstep = 2LL * T;  // words between a query's consecutive key tiles
   constexpr int nks = (hd + 15) >> 4;
 
   float m = -INFINITY;
@@ -581,13 +583,13 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       const auto x0 = __builtin_amdgcn_permlane32_swap(w0, w0, false, false);
       const auto x1 = __builtin_amdgcn_permlane32_swap(w1, w1, false, false);
       if (qok && hl == 0)
-        *(uint2*)(qm + 2 * (k0 / KT)) = make_uint2(w0 | x0[0] | x0[1], w1 | x1[0] | x1[1]);
+        *(uint2*)(qm + tstep * (k0 / KT)) = make_uint2(w0 | x0[0] | x0[1], w1 | x1[0] | x1[1]);
     }
   };
   // the keep words are fetched one tile ahead (tiles above the wave's diagonal read words that
   // were never written; their pairs are causally masked)
   uint2 wn = make_uint2(0, 0);
-  if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * t0);
+  if constexpr (DROP == 2) wn = *(const uint2*)(qm + tstep * t0);
   auto step = [&](auto cur_c, int t) __attribute__((always_inline)) {
     constexpr int CUR = decltype(cur_c)::value;
     const char* Ki = smem + CUR * 2 * IMG;
@@ -597,7 +599,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
     if (more) {  // the other buffer was last read before the previous barrier
       tile_dma(lds0 + (CUR ^ 1) * 2 * IMG, kv, (t + 1) * tstride + kcol, wave_u);
       tile_dma(lds0 + (CUR ^ 1) * 2 * IMG + IMG, kv, (t + 1) * tstride + vcol, wave_u);
-      if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * (t + 1));
+      if constexpr (DROP == 2) wn = *(const uint2*)(qm + tstep * (t + 1));
     }
     const int k0 = t * KT;
     if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
@@ -686,7 +688,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
   const uint32_t tstride = (uint32_t)(KT * ld * 2);
   const uint32_t drow = (uint32_t)bhq;
   const uint32_t hrow = DROP == 1 ? cg_row_hash(seed, drow) : 0u;
-  const uint32_t* qm = DROP == 2 ? qmask + (long long)bhq * wpr : nullptr;
+  const uint32_t* qm = DROP == 2 ? qmask + ((long long)bh * (wpr >> 1) * T + (qok ? myq : 0)) * 2 : nullptr;
+  const long long tstep = 2LL * T;
   constexpr int nks = (hd + 15) >> 4;
   v16f a0 = zero16(), a1 = zero16();
   const int t0 = kmin / KT, t1 = kmax / KT;
@@ -695,7 +698,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
   dma_drain();
   __syncthreads();
   uint2 wn = make_uint2(0, 0);
-  if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * t0);
+  if constexpr (DROP == 2) wn = *(const uint2*)(qm + tstep * t0);
   const RowOff ro = row_offsets(lane);
   const TrOff to = tr_offsets(lane);
   // dP starts from nd = -delta/dscale, added by one MFMA (ones x [hi; lo] split-bf16 nd rows:
@@ -730,7 +733,7 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
     if (more) {  // the other buffer was last read before the previous barrier
       tile_dma(lds0 + (CUR ^ 1) * 2 * IMG, kv, (t + 1) * tstride + kcol, wave_u);
       tile_dma(lds0 + (CUR ^ 1) * 2 * IMG + IMG, kv, (t + 1) * tstride + vcol, wave_u);
-      if constexpr (DROP == 2) wn = *(const uint2*)(qm + 2 * (t + 1));
+      if constexpr (DROP == 2) wn = *(const uint2*)(qm + tstep * (t + 1));
     }
     const int k0 = t * KT;
     // full: every (query, key) of the wave's tile visible.  Otherwise the invisible scores are
@@ -894,6 +897,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
                                                      seg ? T * 4 : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t rqm = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(DROP == 2 ? qmask + bh0 * wpr : nullptr), (short)0, DROP == 2 ? H * T * wpr * 4 : 0, 0x00020000);
+  // this wave's word of key tile mw_idx/2 in the tile-major array: + ((h2*nt + tile)*T + q)*2 + half
   const uint32_t row_lds = (uint32_t)(wave_u < 3 ? 2 * IMG + wave_u * 64 * 4 : BUF - 64 * 4);  // -lse2 | nd | seg
   // iteration cursor: (query head, query tile), advanced without divisions
   struct Cur { int h2, qt; };
@@ -907,7 +911,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     dma4(rrow, buf + row_lds, q < T ? (uint32_t)(((wave_u < 2 ? h2 * T : 0) + q) * 4) : OORD);
     if constexpr (DROP == 2)
       dma4(rqm, buf + (uint32_t)(2 * IMG + 4 * 64 * 4 + wave_u * 64 * 4),
-           (q < T && mw_idx < wpr) ? (uint32_t)(((h2 * T + q) * wpr + mw_idx) * 4) : OORD);
+           (q < T && mw_idx < wpr)
+               ? (uint32_t)((((h2 * (wpr >> 1) + (mw_idx >> 1)) * T + q) * 2 + (mw_idx & 1)) * 4)
+               : OORD);
   };
   // DROP == 1: the row hashes of cu into its buffer's hash slot (after that buffer's DMAs landed)
   auto stage_hash = [&](Cur cu, char* bufp) {

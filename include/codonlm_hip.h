@@ -194,7 +194,7 @@ int cg_attn_fwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
                 int window, uint32_t drop_seed, float drop_p, const void* drop_mask, void* stream);
 /* Attention-dropout keep bits (the same keep(seed, (b*H+h)*T + q, key) as the in-kernel hash),
  * precomputed once per (layer, step) so the bf16 MFMA kernels test one bit per (query, key):
- * a query-major bit array over the causal lower triangle, in a buffer of
+ * a tile-major bit array ([b*H][key tile][query][2 words]) over the causal lower triangle, in a buffer of
  * cg_attn_drop_mask_bytes(B, T, H) bytes.  drop_mask (fwd / bwd): such a buffer made with the
  * same seed and p, or NULL to hash in the kernels (identical keep decisions). */
 size_t cg_attn_drop_mask_bytes(int B, int T, int H);

@@ -418,11 +418,17 @@ def test_attention_bwd_bias_partials(B, T, H, KV, hd, p):
 
 
 def _mask_bits(words, T):
-    """Unpack attn_drop_mask words [BH, T, wpr] (pair-split order) into bool [BH, T, T]."""
-    w = words.cpu().numpy().view(np.uint32)
+    """Unpack attn_drop_mask words -- tile-major [BH, nt, T, 2] (nt = ceil(T/64) key tiles), pair-split
+    bit order -- into bool [BH, T(query), T(key)]."""
+    nt = (T + 63) // 64
+    w = words.cpu().numpy().view(np.uint32).reshape(-1, nt, T, 2)
     i = np.arange(T)
     bit = (i % 32 >> 1) + 16 * (i % 2)
-    return ((w[:, :, i // 32] >> bit.astype(np.uint32)) & 1).astype(bool)
+    half = ((i % 64) // 32)[None, :, None]
+    w0, w1 = w[..., 0], w[..., 1]                                      # [BH, nt, T]
+    wk = np.where(half == 0, w0[:, i // 64, :], w1[:, i // 64, :])      # [BH, key, query]
+    kb = ((wk >> bit.astype(np.uint32)[None, :, None]) & 1).astype(bool)
+    return np.ascontiguousarray(np.transpose(kb, (0, 2, 1)))
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 200, 3), (1, 1024, 2), (1, 64, 1), (1, 129, 1)])
@@ -435,7 +441,7 @@ def test_attn_drop_mask_bits(B, T, H):
     torch.cuda.synchronize()
     wpr = 2 * ((T + 63) // 64)
     assert mask.numel() == B * H * T * wpr
-    qm = _mask_bits(mask.view(B * H, T, wpr), T)        # [bh, q, key]
+    qm = _mask_bits(mask, T)        # [bh, q, key]
     keep = O.dropout_keep(seed, np.arange(B * H * T)[:, None], np.arange(T)[None, :], p).reshape(B * H, T, T)
     causal = np.tril(np.ones((T, T), dtype=bool))[None]
     assert np.array_equal(qm & causal, keep & causal)
@@ -490,8 +496,8 @@ def test_attention_fused_keep_forward(B, T, H, KV, hd, window, sep):
     torch.cuda.synchronize()
     assert torch.equal(y0, y1) and torch.equal(l0, l1)
     wpr = 2 * ((T + 63) // 64)
-    a = _mask_bits(ref.view(B * H, T, wpr), T)
-    b = _mask_bits(mk.view(B * H, T, wpr), T)
+    a = _mask_bits(ref, T)
+    b = _mask_bits(mk, T)
     # visible pairs: causal, same SEP segment (key >= segment start), inside the window
     q = np.arange(T)[:, None]
     k = np.arange(T)[None, :]
