@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void attn_drop_mask_kernel(uint32_t* __restric
 // P, the row sum and the LSE; P <= 256 stays in range).
 // ============================================================================
 // DROP: 0 none, 1 keep bits hashed in the kernel, 2 keep bits read from attn_drop_mask_kernel's
-// query-major words, 3 keep bits hashed in the kernel AND written in those words for the
+// tile-major words, 3 keep bits hashed in the kernel AND written in those words for the
 // backward (what attn_drop_mask_kernel would write for every (query, key) pair a query sees)
 template <int DROP, int HD>
 __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t* __restrict__ qkv, long long ld,
