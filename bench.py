@@ -283,20 +283,13 @@ def main():
         # one kernel template: the persistent fwd/dX GEMM with all its epilogue instantiations, the
         # grouped dW with its tile variants, each attention kernel)
         dominant = max(tuple(L.PROBE_KERNELS), key=lambda k: probes[k][1])
-        if world > 1:  # all ranks probe the same kernel in the timed region
+        if world > 1:  # all ranks probe the same kernel in the probe window
             t = torch.tensor([dominant], device=dev)
             dist.broadcast(t, 0)
             dominant = int(t.item())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    # live HIP events around that class's launches in the timed region, 1 launch in `every`: the
-    # smallest every >= 4 coprime to the class's launches per step, so over the timed steps the
-    # sampled launches cycle through every product of the step (a class spans several shapes)
-    per_step = max(1, probes[dominant][2] // 2) if dominant else 1
-    every = next(e for e in range(4, 64) if math.gcd(e, per_step) == 1)
-    L.lib.cg_probe_sample(every)
-    L.lib.cg_probe_enable(dominant)
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = run(args.warmup + i)
@@ -305,9 +298,22 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # The timed region above carries no probe.  The roofline kernel is then timed live in a
+    # separate window of `probe_steps` further steps: HIP events on the launch stream around 1
+    # launch in `every` of that class -- the smallest every >= 4 coprime to the class's launches
+    # per step, so the sampled launches cycle through every product of the step (a class spans
+    # several shapes).
     live = None
+    per_step = max(1, probes[dominant][2] // 2) if dominant else 1
+    every = next(e for e in range(4, 64) if math.gcd(e, per_step) == 1)
+    probe_steps = max(8, 2 * every)
     if dominant:
         import ctypes as C
+        L.lib.cg_probe_sample(every)
+        L.lib.cg_probe_enable(dominant)
+        for i in range(probe_steps):
+            run(args.warmup + args.steps + i)
+        torch.cuda.synchronize()
         w, ms, k = C.c_double(0), C.c_double(0), C.c_longlong(0)
         L.check(L.lib.cg_probe_read(C.byref(w), C.byref(ms), C.byref(k)), "cg_probe_read")
         nbytes = C.c_double(0)
@@ -357,15 +363,18 @@ def main():
     if rank == 0 and live is not None and live[1] > 0:
         work, ms, k, abytes = live
         ach = work / (ms * 1e-3) / 1e12
-        result["roofline"] = {"kernel": L.PROBE_NAMES[dominant], "rocprof_kernels": L.PROBE_KERNELS[dominant] + "*",
+        result["roofline"] = {"kernel": L.PROBE_NAMES[dominant],
+                              "rocprof_kernels": [p + "*" for p in L.PROBE_KERNELS[dominant]],
                               "bound": "mfma", "achieved": round(ach, 2),
                               "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s", "frac": round(ach / PEAK_BF16_TFLOPS, 4),
                               "traffic": None, "launches": k, "avg_launch_us": round(ms / k * 1e3, 2),
                               "ms_per_step_probe": round(probes[dominant][1] / 2, 3),
                               "algorithmic_bytes_per_launch": round(abytes / k) if k else None,
+                              "launches_per_step": per_step,
                               "measured": f"HIP events on the launch stream around 1 in {every} launches of the "
-                                          f"kernel class ({per_step} launches per step) in the timed region; "
-                                          "achieved = sum of their algorithmic FLOPs (2MNK) / sum of their device time"}
+                                          f"kernel class ({per_step} launches per step) over {probe_steps} steps run "
+                                          "after the timed region (the timed region carries no probe); achieved = "
+                                          "sum of their algorithmic FLOPs (2MNK) / sum of their device time"}
         # HBM bytes per launch of the same kernel class from the committed rocprofv3 PMC passes
         # (FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections; tools/pmc_traffic.py); attached only for
         # the same config, batch and kernel class, newest round first, with the commit the counters

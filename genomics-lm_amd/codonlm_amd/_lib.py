@@ -29,9 +29,12 @@ PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", P
                PROBE_GEMM_PERS: "gemm_bf16_pers"}
 # rocprofv3 kernel-name prefixes of the probed kernel classes (every instantiation whose name
 # starts with the prefix belongs to the class; bench.py / tools/kstats.py sum them)
-PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: "gemm_dw_kernel", PROBE_ATTN_FWD: "attn_fwd_mfma",
-                 PROBE_ATTN_DQ: "attn_bwd_dq_mfma", PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma",
-                 PROBE_GEMM_PERS: "gemm_bf16_pers_kernel"}
+PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: ("gemm_dw_kernel",), PROBE_ATTN_FWD: ("attn_fwd_mfma",),
+                 PROBE_ATTN_DQ: ("attn_bwd_dq_mfma",), PROBE_ATTN_DKDV: ("attn_bwd_dkdv_mfma",),
+                 # the persistent forward / dX class: the eight-wave kernel and its loader-wave
+                 # variant (plain and bias-only products), both launched through cg_gemm's
+                 # persistent path and probed together
+                 PROBE_GEMM_PERS: ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel")}
 
 # parameter kinds (enum in the header)
 (P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,
@@ -112,7 +115,8 @@ class Model(C.Structure):
                 ("idx", vp), ("targets", vp), ("logits", vp),
                 ("aux_ready", i32), ("head_grad_scale", f32), ("head_grad_scale_dev", vp), ("d_term_logits", vp),
                 ("ld_d_term", i64),
-                ("d_offset_logits", vp * 8), ("dw_done_layer", i32)]
+                ("d_offset_logits", vp * 8), ("dw_done_layer", i32),
+                ("head_dw_off", i64), ("head_dw_alpha", f32), ("head_dw_accumulate", i32), ("head_dw_pending", i32)]
 
 
 # name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
@@ -122,6 +126,7 @@ SIGNATURES = {
     "cg_gemm_set_pers": (i32, [i32]),
     "cg_set_cu_reserve": (i32, [i32]),
     "cg_gemm_set_pers_lw": (i32, [i32]),
+    "cg_set_head_dw_defer": (i32, [i32]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),
     "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),

@@ -43,10 +43,13 @@ def bucket_ranges(model):
 class DataParallelStep:
     """fwd + CE + bwd (+ bucketed all-reduce) + AdamW for one microbatch group."""
 
-    def __init__(self, model, optimizer, group=None):
+    def __init__(self, model, optimizer, group=None, always_reduce: bool = False):
+        """``always_reduce``: issue the bucket all-reduces even at world size 1 (an identity
+        over one rank) -- the single-GPU smoke of the RCCL path (tests/test_gpu_rccl.py)."""
         self.model = model
         self.opt = optimizer
         self.group = group
+        self.always_reduce = always_reduce
         on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if on else 1
         self.rank = dist.get_rank(group) if on else 0
@@ -56,7 +59,7 @@ class DataParallelStep:
         grads = self.model.flat_grads()
 
         def hook(name):
-            if self.world <= 1:
+            if self.world <= 1 and not self.always_reduce:
                 return
             b, e = self.ranges[name]
             if e > b:

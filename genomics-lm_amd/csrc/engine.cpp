@@ -612,26 +612,20 @@ int head_dw_now(const Ctx& C, long long hoff, float alpha, int accumulate) {
 // launch (bf16, no aux heads): a few more tiles beside the group's (the C4 remainder group fills
 // 192 of 256 CUs) instead of a split-K product (22 us) and its slab reduction (7 us).  Its
 // operands (dlogits, xf) are not written again before that launch, and the tied gradient
-// (tok_emb) is final only after phase 2, so no data-parallel bucket sees it early.  Keyed by
-// model like the pending reductions; phase 0 (re)sets it, phase 2 runs it if no group did.
-struct HeadDw {
-  const cg_model* m;
-  long long hoff;
-  float alpha;
-  int accumulate;
-  bool on;
-};
-HeadDw& head_dw_pending(const cg_model* m) {
-  static std::vector<HeadDw> v;
-  for (auto& e : v)
-    if (e.m == m) return e;
-  v.push_back(HeadDw{m, 0, 1.0f, 0, false});
-  return v.back();
-}
+// (tok_emb) is final only after phase 2, so no data-parallel bucket sees it early.  The pending
+// product lives in the cg_model itself (head_dw_*), so its lifetime and thread ownership are the
+// model's; phase 0 (re)sets it, phase 2 runs it if no group did.
 static int g_head_dw_defer = [] {
   const char* e = getenv("CG_HEAD_DW_DEFER");
   return e ? atoi(e) : 1;
 }();
+}  // namespace
+extern "C" int cg_set_head_dw_defer(int on) {
+  const int prev = g_head_dw_defer;
+  g_head_dw_defer = on ? 1 : 0;
+  return prev;
+}
+namespace {
 
 // The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
 // bf16 mode (gemm_dw.h), the per-product GEMMs in fp32 parity mode.
@@ -666,15 +660,15 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
     CK(add(sl.gattn, d, a.y, d, o.wp));
     CK(add(sl.dqkv, D.Nqkv, a.h1, d, o.wqkv));
   }
-  HeadDw& hd = head_dw_pending(C.m);
-  if (hd.on && C.dt == CG_BF16 && grp.n < CG_DW_MAX) {
+  cg_model* mm = const_cast<cg_model*>(C.m);
+  if (mm->head_dw_pending && C.dt == CG_BF16 && grp.n < CG_DW_MAX) {
     cg_dw_product& q = grp.p[grp.n++];
     q.A = C.A.dlogits; q.lda = C.A.ldl;
     q.B = C.A.xf; q.ldb = d;
-    q.C = G(C, hd.hoff); q.ldc = d;
+    q.C = G(C, mm->head_dw_off); q.ldc = d;
     q.N_out = D.Vp; q.K_out = d;
-    q.alpha = hd.alpha; q.accumulate = hd.accumulate;
-    hd.on = false;
+    q.alpha = mm->head_dw_alpha; q.accumulate = mm->head_dw_accumulate;
+    mm->head_dw_pending = 0;
   }
   if (C.dt == CG_BF16 && grp.n) return cg_gemm_dw_grouped(&grp, C.s);
   return CG_OK;
@@ -709,7 +703,6 @@ int aux_backward(const Ctx& C, int accumulate) {
       g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
       g.split_k = pick_split(C, ncp, d, M);
       g.workspace = A.splitws;
-    g.ws_bytes = A.nb.splitws;
       g.ws_bytes = A.nb.splitws;
       CK(cg_gemm(&g, C.s));
       CK(cg_colsum(CG_F32, m->d_term_logits, m->ld_d_term, (int)M, nc, G(C, C.Lo.termb), accumulate, A.colws,
@@ -1049,14 +1042,18 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (m->targets && m->head_grad_scale_dev)  // d(objective)/d(loss) still on the device
       CK(cg_scale_dev(C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.dlogits, A.ldl, (int)M, D.Vp, m->head_grad_scale_dev,
                       C.s));
-    HeadDw& hd = head_dw_pending(m);
-    hd.on = false;
+    m->head_dw_pending = 0;
     if (m->targets) {
       // d(head weight) = s dlogits^T . xf: deferred into the first dW group when nothing else
       // adds into it before that launch (the aux heads do, and reuse dlogits)
       if (g_head_dw_defer && C.dt == CG_BF16 && D.L > 0 && m->cfg.tie_embeddings && !m->cfg.termination_aux &&
           m->cfg.n_offsets <= 0)
-        hd = HeadDw{m, hoff, m->head_grad_scale, accumulate, true};
+      {
+        m->head_dw_off = hoff;
+        m->head_dw_alpha = m->head_grad_scale;
+        m->head_dw_accumulate = accumulate;
+        m->head_dw_pending = 1;
+      }
       else
         CK(head_dw_now(C, hoff, m->head_grad_scale, accumulate));
       // dxf = s dlogits . E
@@ -1163,10 +1160,9 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
   }
   if (phase == 2) {
     CK(flush_reduce(m, C.s));  // nothing is pending after block 0; kept for partial phase sequences
-    HeadDw& hd = head_dw_pending(m);
-    if (hd.on) {  // a partial phase sequence: no dW group took the head's product
-      hd.on = false;
-      CK(head_dw_now(C, hd.hoff, hd.alpha, hd.accumulate));
+    if (m->head_dw_pending) {  // a partial phase sequence: no dW group took the head's product
+      m->head_dw_pending = 0;
+      CK(head_dw_now(C, m->head_dw_off, m->head_dw_alpha, m->head_dw_accumulate));
     }
     // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
     const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
@@ -1362,4 +1358,4 @@ extern "C" int cg_model_decode(cg_model* m, const int64_t* tok, int B, int pos, 
   return CG_OK;
 }
 
-extern "C" const char* cg_version(void) { return "codonlm_hip 0.1 gfx950"; }
+extern "C" const char* cg_version(void) { return "codonlm_hip 0.3 gfx950"; }

@@ -1506,7 +1506,7 @@ __device__ __forceinline__ void adamw_elem(float& pi, float gi, float& mi, float
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                     float* __restrict__ m, float* __restrict__ v,
                                                     bf16_t* __restrict__ shadow, AdamSegs segs, float b1, float b2,
-                                                    float eps, float bc1, float bc2_sqrt, float gscale) {
+                                                    float eps, float bc1, float bc2_sqrt, float gscale, int vec) {
   const long long tid = blockIdx.x * 256ll + threadIdx.x, nth = (long long)gridDim.x * 256;
   for (int si = 0; si < segs.n; ++si) {
     const long long b = segs.begin[si], e = segs.end[si];
@@ -1521,7 +1521,7 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
       p[i] = pi;
       if (shadow) shadow[i] = f2bf(pi);
     };
-    if (a0 >= a1) {
+    if (!vec || a0 >= a1) {  // !vec: a base pointer the 16-B (shadow: 8-B) accesses cannot use
       for (long long i = b + tid; i < e; i += nth) one(i);
       continue;
     }
@@ -1560,8 +1560,13 @@ extern "C" int cg_adamw(float* param, const float* grad, float* exp_avg, float* 
   int blocks = (int)((total + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   if (blocks < 1) blocks = 1;
+  // the float4 / packed-bf16 interior needs 16-B aligned fp32 bases and an 8-B aligned shadow
+  // (the engine's flat buffers are; an offset view through the C ABI may not be)
+  auto al = [](const void* q, uintptr_t a) { return ((uintptr_t)q & (a - 1)) == 0; };
+  const int vec = al(param, 16) && al(grad, 16) && al(exp_avg, 16) && al(exp_avg_sq, 16) &&
+                  (!shadow_bf16 || al(shadow_bf16, 8));
   hipLaunchKernelGGL(adamw_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, param, grad, exp_avg, exp_avg_sq,
-                     (bf16_t*)shadow_bf16, s, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), grad_scale);
+                     (bf16_t*)shadow_bf16, s, beta1, beta2, eps, (float)bc1, (float)sqrt(bc2), grad_scale, vec);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }

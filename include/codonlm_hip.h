@@ -392,6 +392,13 @@ typedef struct {
    * gradient of blocks >= dw_done_layer (and of the head / ln_f after phase 0) is final --
    * the point a data-parallel caller may start that bucket's all-reduce. */
   int dw_done_layer;
+  /* engine-private backward state (zero-initialise; the caller never writes it): the tied
+   * head's weight gradient deferred from phase 0 into the first grouped dW launch (bf16, tied,
+   * no aux heads).  Phase 0 sets it, the first dW group or phase 2 consumes it. */
+  long long head_dw_off;
+  float head_dw_alpha;
+  int head_dw_accumulate;
+  int head_dw_pending;
 } cg_model;
 
 /* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
@@ -474,6 +481,14 @@ int cg_probe_bytes(double* bytes);
  * all-reduce) when measuring the persistent launches' sensitivity to busy CUs */
 int cg_diag_occupy(int n_cus, int usec, void* stream);
 
+/* the tied head's weight gradient (bf16, tied, no aux heads) deferred from backward phase 0
+ * into the first grouped dW launch: 1 (default; env CG_HEAD_DW_DEFER at load) or 0 (a split-K
+ * product in phase 0).  Returns the previous setting. */
+int cg_set_head_dw_defer(int on);
+
+/* "codonlm_hip <abi> gfx950".  ABI 0.2 (round 3): cg_gemm_desc.ws_bytes and the size_t
+ * workspace-size argument after every workspace pointer.  ABI 0.3 (round 4): cg_model gained
+ * the engine-private head_dw_* fields at its end. */
 const char* cg_version(void);
 
 #ifdef __cplusplus

@@ -1,0 +1,73 @@
+"""The tied head's weight gradient, deferred from backward phase 0 into the first grouped dW
+launch (engine.cpp flush_dw): deferral on vs off, and the phase-2 fallback of a
+partial phase sequence (phase 0 then phase 2, no dW group to take the product).
+
+Reference: the head is tied to tok_emb (model_tiny_gpt.py:217-219), so d(tok_emb) = the head's
+dlogits^T . ln_f(x) plus the embedding scatter-add (loss.backward(), loop.py:1233).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _model(seed=7):
+    from codonlm_amd import TinyGPT
+    torch.manual_seed(seed)
+    m = TinyGPT(68, 128, n_layer=3, n_head=4, n_embd=128, dropout=0.0, label_smoothing=0.05,
+                compute_dtype="bf16", device=DEV)
+    m.train()
+    return m
+
+
+def _batch(B=4, T=128, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    t = torch.randint(4, 68, (B, T + 1), generator=g)
+    t[:, 40] = 3  # a SEP segment
+    return t[:, :-1].to(DEV), t[:, 1:].to(DEV)
+
+
+def _grads(defer, partial):
+    from codonlm_amd import _lib as L
+    old = L.lib.cg_set_head_dw_defer(int(defer))
+    try:
+        m = _model()
+        x, y = _batch()
+        m.flat_grads().zero_()
+        _, loss = m(x, y)
+        if partial:
+            eng = m.engine
+            eng.set_head_grads(1.0)
+            eng.backward_phase(0, 0, False)
+            eng.backward_phase(2, 0, False)
+        else:
+            loss.backward()
+        torch.cuda.synchronize()
+        return {k: v.grad.detach().clone() for k, v in m.named_parameters() if v.grad is not None}
+    finally:
+        L.lib.cg_set_head_dw_defer(old)
+
+
+def _rel(a, b):
+    return float((a - b).norm() / max(float(b.norm()), 1e-30))
+
+
+def test_head_dw_defer_on_equals_off():
+    on, off = _grads(True, False), _grads(False, False)
+    assert on.keys() == off.keys()
+    # tok_emb: the same fp32-accumulated product over the same bf16 operands in another
+    # summation order (grouped dW tile vs split-K slabs)
+    assert _rel(on["tok_emb.weight"], off["tok_emb.weight"]) < 1e-5
+    for k in on:
+        if k != "tok_emb.weight":
+            assert _rel(on[k], off[k]) < 1e-6, k
+
+
+def test_head_dw_partial_phases_runs_deferred_product():
+    """phase 0 then phase 2: with deferral on, no dW group took the head's product, so phase 2
+    must run it -- tok_emb.grad equals the non-deferred sequence's."""
+    on, off = _grads(True, True), _grads(False, True)
+    te_on, te_off = on["tok_emb.weight"], off["tok_emb.weight"]
+    assert float(te_off.abs().max()) > 0
+    assert _rel(te_on, te_off) < 1e-5

@@ -597,6 +597,29 @@ def test_adamw_matches_torch():
     assert (shadow.float().cpu() - ps.detach()).abs().max() < 1e-2
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_adamw_offset_views(shift):
+    """Offset views through the C ABI (bases not 16-B / 8-B aligned) take the elementwise path
+    and give the aligned result bit for bit (the float4 interior needs aligned bases)."""
+    ops = _ops()
+    n = 5001
+    g = torch.Generator().manual_seed(50 + shift)
+    p0, grad = torch.randn(n, generator=g), torch.randn(n, generator=g)
+    outs = []
+    for off in (0, shift):
+        bufs = [torch.zeros(n + 8, device=DEV) for _ in range(4)]
+        pd, gd, m, v = (b[off:off + n] for b in bufs)
+        pd.copy_(p0.to(DEV))
+        gd.copy_(grad.to(DEV))
+        sh = torch.zeros(n + 8, dtype=torch.bfloat16, device=DEV)[off:off + n]
+        for step in (1, 2):
+            ops.adamw_(pd, gd, m, v, step, [(0, 1000, 1e-3, 0.05), (1000, n, 2e-3, 0.0)], shadow=sh, grad_scale=0.5)
+        torch.cuda.synchronize()
+        outs.append((pd.cpu().clone(), m.cpu().clone(), v.cpu().clone(), sh.float().cpu().clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 512), (1000, 200, 192), (256, 136, 1024)])
