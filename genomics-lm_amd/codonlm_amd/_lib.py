@@ -31,10 +31,11 @@ PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", P
 # starts with the prefix belongs to the class; bench.py / tools/kstats.py sum them)
 PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: ("gemm_dw_kernel",), PROBE_ATTN_FWD: ("attn_fwd_mfma",),
                  PROBE_ATTN_DQ: ("attn_bwd_dq_mfma",), PROBE_ATTN_DKDV: ("attn_bwd_dkdv_mfma",),
-                 # the persistent forward / dX class: the eight-wave kernel and its loader-wave
-                 # variant (plain and bias-only products), both launched through cg_gemm's
-                 # persistent path and probed together
-                 PROBE_GEMM_PERS: ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel")}
+                 # the persistent forward / dX class: the eight-wave kernel, its loader-wave variant
+                 # (plain and bias-only products) and the ping-pong variants (gemm_pp.h, gemm_pp2.h;
+                 # off by default), all launched through cg_gemm's persistent path, probed together
+                 PROBE_GEMM_PERS: ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel", "gemm_bf16_pp_kernel",
+                                   "gemm_bf16_pp2_kernel")}
 
 # parameter kinds (enum in the header)
 (P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,
@@ -126,6 +127,8 @@ SIGNATURES = {
     "cg_gemm_set_pers": (i32, [i32]),
     "cg_set_cu_reserve": (i32, [i32]),
     "cg_gemm_set_pers_lw": (i32, [i32]),
+    "cg_gemm_set_pers_pp": (i32, [i32]),
+    "cg_gemm_set_pers_pp2": (i32, [i32]),
     "cg_set_head_dw_defer": (i32, [i32]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),

@@ -556,6 +556,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
 #include "gemm_wide.h"
 #include "gemm_pers.h"
 #include "gemm_lw.h"
+#include "gemm_pp.h"
+#include "gemm_pp2.h"
 #include "gemm_dw.h"
 
 // CG_EPI_COLSUM fallback: part[r/64][n] = sum of C rows [64r, 64r+64) (column n)
@@ -635,14 +637,59 @@ extern "C" int cg_gemm_set_pers_lw(int mode) {
   g_pers_lw = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
   return old;
 }
+// the ping-pong kernel (gemm_pp.h): 0 off, 1 (env CG_PERS_PP at load) for products without an
+// epilogue or with a bias only, 2 for every epilogue
+static int g_pers_pp = [] {
+  const char* e = getenv("CG_PERS_PP");
+  return e ? atoi(e) : 0;
+}();
+extern "C" int cg_gemm_set_pers_pp(int mode) {
+  const int old = g_pers_pp;
+  g_pers_pp = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
+  return old;
+}
+static bool pers_pp_for(int e) {
+  if (g_pers_pp == 2) return true;
+  return g_pers_pp == 1 && (e == 0 || e == CG_EPI_BIAS);
+}
 // the SwiGLU backward's epilogue does not fit the loader-wave kernel's 168-register budget
 static bool pers_lw_for(int e) {
+  if (pers_pp_for(e)) return false;
   if (g_pers_lw == 2) return e != CG_EPI_DSWIGLU;
   return g_pers_lw == 1 && (e == 0 || e == CG_EPI_BIAS);
 }
+// the 256x256 ping-pong kernel (gemm_pp2.h) for bf16-output products with at least one 256-wide
+// column tile per CU-round: 0 off, 1 (env CG_PERS_PP2 at load)
+static int g_pers_pp2 = [] {
+  const char* e = getenv("CG_PERS_PP2");
+  return e ? atoi(e) : 0;
+}();
+extern "C" int cg_gemm_set_pers_pp2(int mode) {
+  const int old = g_pers_pp2;
+  g_pers_pp2 = mode < 0 ? 0 : (mode > 1 ? 1 : mode);
+  return old;
+}
+static gemm_kernel_t pick_pp2(int e, int ct) {
+  if (ct != CG_BF16) return nullptr;
+#define P2SPEC(E) \
+  if (e == (E)) return gemm_bf16_pp2_kernel<(E)>;
+  P2SPEC(0)
+  P2SPEC(CG_EPI_BIAS)
+  P2SPEC(CG_EPI_BIAS | CG_EPI_GELU)
+  P2SPEC(CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV)
+  P2SPEC(CG_EPI_DGELU)
+  P2SPEC(CG_EPI_DGELU | CG_EPI_GELU_DERIV)
+  P2SPEC(CG_EPI_DGELU | CG_EPI_COLSUM)
+  P2SPEC(CG_EPI_DGELU | CG_EPI_GELU_DERIV | CG_EPI_COLSUM)
+  P2SPEC(CG_EPI_COLSUM)
+#undef P2SPEC
+  return nullptr;
+}
 static gemm_kernel_t pick_pers(int e, int ct) {
-#define PSPEC(E, T) \
-  if (e == (E) && ct == (T)) return pers_lw_for(e) ? gemm_bf16_lw_kernel<(E), (T)> : gemm_bf16_pers_kernel<(E), (T)>;
+#define PSPEC(E, T)                                                                              \
+  if (e == (E) && ct == (T))                                                                    \
+    return pers_pp_for(e) ? gemm_bf16_pp_kernel<(E), (T)>                                       \
+                          : pers_lw_for(e) ? gemm_bf16_lw_kernel<(E), (T)> : gemm_bf16_pers_kernel<(E), (T)>;
   PSPEC(0, CG_BF16)
   PSPEC(0, CG_F32)
   PSPEC(CG_EPI_BIAS, CG_BF16)
@@ -826,13 +873,24 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     if (swg && !pers) return CG_EUNSUPPORTED;
     if (!pers) p.epi &= ~CG_EPI_COLSUM;  // only the persistent tile fuses the column sums
     const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
-    if (pers) {
+    // 256x256 tiles: the products with N >= 1024 (at M = B.T >= 4096 at least one round of
+    // 256-wide tiles over the CUs) -- see gemm_pp2.h
+    const bool pp2 = pers && g_pers_pp2 && pick_pp2(p.epi, p.c_dtype) && p.N >= 1024 && p.K % bp2::BK == 0 &&
+                     (long long)cg_cdiv(p.M, bp2::BM) * cg_cdiv(p.N, bp2::BN) >= cg_pers_cus();
+    if (pp2) {
+      k = pick_pp2(p.epi, p.c_dtype);
+      colsum_fused = colsum;
+      const int tiles = cg_cdiv(p.N, bp2::BN) * cg_cdiv(p.M, bp2::BM);
+      g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cg_pers_cus()));
+      blk = dim3(bp2::THREADS);
+      sh = bp2::SMEM;
+    } else if (pers) {
       k = pick_pers(p.epi, p.c_dtype);
       colsum_fused = colsum;
       const int tiles = cg_cdiv(p.N, (p.epi & CG_EPI_SWIGLU) ? bfp::BN / 2 : bfp::BN) * cg_cdiv(p.M, bfp::BM);
       g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cg_pers_cus()));
-      blk = dim3(pers_lw_for(p.epi) ? bfl::THREADS : bfp::THREADS);
-      sh = bfp::SMEM;
+      blk = dim3(pers_pp_for(p.epi) ? bpp::THREADS : pers_lw_for(p.epi) ? bfl::THREADS : bfp::THREADS);
+      sh = pers_pp_for(p.epi) ? bpp::SMEM : bfp::SMEM;
     } else if (vec && use_wide(d, kchunk, split)) {
       k = pick_spec<WideK>(d->a_kcontig, d->b_kcontig, ke, kt);
       g = dim3(cg_cdiv(p.N, bfw::BN) * cg_cdiv(p.M, bfw::BM) * split);

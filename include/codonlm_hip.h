@@ -89,6 +89,14 @@ int cg_set_cu_reserve(int n);
  * CG_PERS_LW at load) for products without an epilogue or with a bias only, 2 wherever it
  * implements the epilogue.  Returns the previous mode. */
 int cg_gemm_set_pers_lw(int mode);
+/* persistent-tile variant in which the two waves of each SIMD alternate MFMA and load segments
+ * (gemm_pp.h): 0 off (default; env CG_PERS_PP at load), 1 for products without an epilogue or
+ * with a bias only, 2 for every epilogue.  Takes precedence over the loader-wave variant.
+ * Returns the previous mode. */
+int cg_gemm_set_pers_pp(int mode);
+/* 256x256-tile ping-pong variant (gemm_pp2.h) for bf16-output products with N >= 1024 and at
+ * least one tile per CU: 0 off (default; env CG_PERS_PP2 at load), 1 on.  Returns the previous mode. */
+int cg_gemm_set_pers_pp2(int mode);
 int cg_pers_cus(void);
 
 /* Grouped weight-gradient GEMM: for every product p of the group

@@ -186,14 +186,23 @@ def test_swiglu_fwd_bwd(dtype, H, Hp, ld_pad):
     assert torch.all(d[:, H:Hp] == 0) and torch.all(d[:, Hp + H:] == 0)
 
 
+@pytest.mark.parametrize("pp", [0, 2])
 @pytest.mark.parametrize("M,Hp,H,K", [(1024, 1024, 1024, 384), (700, 1408, 1365, 512), (256, 128, 100, 128)])
-def test_gemm_swiglu_epilogues(M, Hp, H, K):
+def test_gemm_swiglu_epilogues(M, Hp, H, K, pp):
     """The gate|up product with SwiGLU in the persistent tile's epilogue (CG_EPI_SWIGLU: B rows
     remapped so one lane holds gate j and up j) and the dL/ds product with the SwiGLU backward in
     its epilogue (CG_EPI_DSWIGLU), against the separate passes (cg_swiglu_fwd / _bwd) on the same
     bf16 products."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
+    old_pp = L.lib.cg_gemm_set_pers_pp(pp)
+    try:
+        _swiglu_epilogues(ops, L, M, Hp, H, K)
+    finally:
+        L.lib.cg_gemm_set_pers_pp(old_pp)
+
+
+def _swiglu_epilogues(ops, L, M, Hp, H, K):
     g = torch.Generator().manual_seed(M + Hp)
     x = (torch.randn(M, K, generator=g) * 0.5).to(DEV, torch.bfloat16)
     wgu = torch.randn(2 * Hp, K, generator=g) * K ** -0.5
@@ -660,7 +669,7 @@ def test_transpose16_batch():
         assert torch.equal(o.cpu(), m.cpu().t())
 
 
-@pytest.mark.parametrize("lw", [0, 1, 2])
+@pytest.mark.parametrize("lw", [0, 1, 2, 3])
 @pytest.mark.parametrize("cap", [1, 3])
 @pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256), (600, 200, 320),
                                    (520, 264, 512)])
@@ -671,7 +680,7 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     192 issue the epilogue loads in the last k-step; K = 256 / 320 / 512 spread them over the
     tile's last 1 / 2 / 4 k-steps.  CG_EPI_GELU_DERIV: the forward stores gelu'(pre) and the
     backward multiplies by it.  lw=2: the same on the loader-wave variant (gemm_lw.h) for every
-    epilogue it implements."""
+    epilogue it implements.  lw=3: the ping-pong variant (gemm_pp.h) for every epilogue."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
     g = torch.Generator().manual_seed(M + N + K)
@@ -683,7 +692,8 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     base = _bf(x) @ _bf(w).t()
     tol = 3e-2 * 4
     old = L.lib.cg_gemm_set_pers(cap)
-    old_lw = L.lib.cg_gemm_set_pers_lw(lw)
+    old_lw = L.lib.cg_gemm_set_pers_lw(lw if lw < 3 else 0)
+    old_pp = L.lib.cg_gemm_set_pers_pp(2 if lw == 3 else 0)
     try:
         y0 = ops.gemm(xd, wd, out_dtype=torch.float32)
         y0b = ops.gemm(xd, wd, out_dtype=torch.bfloat16)
@@ -713,6 +723,7 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     finally:
         L.lib.cg_gemm_set_pers(old)
         L.lib.cg_gemm_set_pers_lw(old_lw)
+        L.lib.cg_gemm_set_pers_pp(old_pp)
     pre = base + bias
     assert (y0.cpu() - base).abs().max() < tol
     assert (y0b.float().cpu() - base).abs().max() < tol + 0.01 * base.abs().max()
@@ -739,6 +750,63 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     assert (ydgd.float().cpu() - ref_dgd).abs().max() < tol + 0.01 * base.abs().max()
     assert torch.equal(ydcd.cpu(), ydgd.cpu())
     assert (csd.cpu() - ref_dgd.sum(0)).abs().max() < 1e-2 * (1 + ref_dgd.abs().sum(0).max())
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+@pytest.mark.parametrize("M,N,K", [(8192, 2048, 512), (8000, 2100, 128), (4096, 4160, 256)])
+def test_gemm_pp2_epilogues(cap, M, N, K):
+    """The 256x256 ping-pong tile (gemm_pp2.h; N >= 1024, at least one tile per CU) for every
+    epilogue it implements, partial M / N tiles, K = 128 / 256 / 512 (4 / 8 / 16 k-steps of 32),
+    and (cap = 3) three workgroups that each walk ~100 tiles, so the 4-stage ring and its counted
+    waits cross many tile seams with epilogue stores in flight.  Each result against the
+    persistent 256x128 tile on the same bf16 operands (same fp32 products, different summation
+    order) and fp32 torch."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    g = torch.Generator().manual_seed(M + N + K)
+    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(DEV, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(DEV)
+    aux = (torch.randn(M, N, generator=g) * 0.5).to(DEV, torch.bfloat16)
+
+    def run(pp2):
+        old = L.lib.cg_gemm_set_pers(cap)
+        old2 = L.lib.cg_gemm_set_pers_pp2(pp2)
+        try:
+            out = {}
+            out["plain"] = ops.gemm(x, w, out_dtype=torch.bfloat16)
+            out["bias"] = ops.gemm(x, w, out_dtype=torch.bfloat16, bias=bias, epilogue=L.EPI_BIAS)
+            a1 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            out["gelu"] = ops.gemm(x, w, out_dtype=torch.bfloat16, bias=bias, epilogue=L.EPI_BIAS | L.EPI_GELU,
+                                   aux_out=a1)
+            out["gelu_pre"] = a1
+            a2 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            out["gelud"] = ops.gemm(x, w, out_dtype=torch.bfloat16, bias=bias,
+                                    epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_DERIV, aux_out=a2)
+            out["gelud_d"] = a2
+            out["dgelu"] = ops.gemm(x, w, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux)
+            out["dgelud"] = ops.gemm(x, w, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=aux)
+            cs = torch.empty(N, device=DEV)
+            out["dgeludc"] = ops.gemm(x, w, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV,
+                                      aux=aux, colsum_out=cs)
+            out["cs"] = cs
+            cs2 = torch.empty(N, device=DEV)
+            out["plainc"] = ops.gemm(x, w, out_dtype=torch.bfloat16, colsum_out=cs2)
+            out["cs2"] = cs2
+            torch.cuda.synchronize()
+            return out
+        finally:
+            L.lib.cg_gemm_set_pers(old)
+            L.lib.cg_gemm_set_pers_pp2(old2)
+
+    got, ref = run(1), run(0)
+    base = x.float() @ w.float().t()
+    assert (got["plain"].float() - base).abs().max().item() <= 2e-2 * (1 + base.abs().max().item())
+    for key in got:
+        a, b = got[key].float(), ref[key].float()
+        tol = 1e-3 if key in ("cs", "cs2") else 1.6e-2
+        err = (a - b).abs().max().item()
+        assert err <= tol * (1 + b.abs().max().item()), (key, err)
 
 
 @pytest.mark.parametrize("dtype,pers", [(torch.float32, 1), (torch.bfloat16, 0), (torch.bfloat16, 1)])

@@ -95,16 +95,38 @@ def main():
         if f0:
             f0()
     torch.cuda.synchronize()
-    best = {}
     only = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] else None  # e.g. "fc2 dX": time only matching rows
     rows = [r for r in rows if only is None or r[0].startswith(only)]
+    # GEMM_VARIANTS="base,pp1,pp2,pp1+pp2": the persistent-tile variants to interleave
+    # (base: neither ping-pong kernel; ppN: cg_gemm_set_pers_pp(N); pp2: cg_gemm_set_pers_pp2(1))
+    import os
+
+    def set_variant(v):
+        parts = v.split("+")
+        L.lib.cg_gemm_set_pers_pp(next((int(t[2:]) for t in parts if t.startswith("pp") and t != "pp2"), 0))
+        L.lib.cg_gemm_set_pers_pp2(1 if "pp2" in parts else 0)
+
+    modes = [v for v in os.environ.get("GEMM_VARIANTS", "").split(",") if v] or [None]
+    bests = {m: {} for m in modes}
     for _ in range(8):
-        for name, _, _, f, f0 in rows:
-            for tag, fn in (("epi", f), ("plain", f0)):
-                if fn is None:
-                    continue
-                t = timer(fn)
-                best[(name, tag)] = min(best.get((name, tag), 1e9), t)
+        for mode in modes:
+            if mode is not None:
+                set_variant(mode)
+            best = bests[mode]
+            for name, _, _, f, f0 in rows:
+                for tag, fn in (("epi", f), ("plain", f0)):
+                    if fn is None:
+                        continue
+                    t = timer(fn)
+                    best[(name, tag)] = min(best.get((name, tag), 1e9), t)
+    for mode in modes:
+        if mode is not None:
+            set_variant(mode)
+            print(f"== persistent variant: {mode}")
+        report(rows, bests[mode], only)
+
+
+def report(rows, best, only):
     tot = 0.0
     for name, N, K, f, f0 in rows:
         fl = 2.0 * M * N * K
