@@ -14,7 +14,11 @@ Batch ORDER is the reference's, bit for bit:
   * ``bucket_batching`` on dynamic data: BucketBatchSampler (:332-377) restated;
   * val loader: sequential, unshuffled.
 Storage formats: fixed windows (NPZ ``X``/``Y`` [N, T]) or dynamic sequences (NPZ flat
-``X`` + ``lengths``), loaded with ``allow_pickle=False`` like the reference.
+``X`` + ``lengths``), loaded with ``allow_pickle=False`` like the reference.  With ``use_mmap``
+(the reference's MmapPackedDataset, data_loading.py:132-200) uncompressed ``<stem>_X.npy`` /
+``_Y.npy`` / ``_lengths.npy`` sidecars are memory-mapped and streamed to HBM in chunks, so the
+corpus is never materialised in host RAM; without sidecars the NPZ is read, as the reference's
+fallback does.
 """
 from __future__ import annotations
 
@@ -30,6 +34,62 @@ PAD_ID = 0
 _ELEM = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}
 
 
+_CHUNK = 1 << 24  # elements per host->device piece of a memory-mapped array
+
+
+def _width_for(lo: int, hi: int, dtype: np.dtype) -> int:
+    if dtype.itemsize == 1 and dtype.kind == "u":
+        return 1
+    if lo >= -(1 << 15) and hi < (1 << 15) and dtype.itemsize <= 2:
+        return 2
+    if lo >= -(1 << 31) and hi < (1 << 31) and dtype.itemsize <= 4:
+        return 4
+    return 8
+
+
+def _device_int_stream(a: np.ndarray, device) -> tuple[torch.Tensor, int]:
+    """_device_int for a memory-mapped array: min / max and the upload in _CHUNK pieces (one
+    pinned staging buffer), never the whole array in host memory."""
+    if a.dtype.kind not in "iu":
+        raise TypeError(f"token arrays must be integer, got {a.dtype}")
+    flat = a.reshape(-1)
+    if flat.size == 0:
+        return torch.zeros(a.shape, dtype=torch.int32, device=device), 4
+    lo, hi = None, None
+    for i in range(0, flat.size, _CHUNK):
+        c = flat[i:i + _CHUNK]
+        clo, chi = int(c.min()), int(c.max())
+        lo = clo if lo is None else min(lo, clo)
+        hi = chi if hi is None else max(hi, chi)
+    eb = _width_for(lo, hi, a.dtype)
+    nd = _ELEM[eb]
+    out = torch.empty(flat.size, dtype=torch.from_numpy(np.zeros(0, nd)).dtype, device=device)
+    stage = torch.empty(min(_CHUNK, flat.size), dtype=out.dtype, pin_memory=torch.cuda.is_available())
+    for i in range(0, flat.size, _CHUNK):
+        c = np.asarray(flat[i:i + _CHUNK]).astype(nd, copy=False)
+        st = stage[:len(c)]
+        st.numpy()[:] = c
+        out[i:i + len(c)].copy_(st, non_blocking=False)
+    return out.view(a.shape), eb
+
+
+def _npy_sidecars(paths):
+    """The reference's MmapPackedDataset probe (data_loading.py:142-158): per path the
+    ``<stem>_X.npy`` and ``_Y.npy`` or ``_lengths.npy`` sidecars, or None if any path lacks them."""
+    from pathlib import Path
+    out = []
+    for path in paths:
+        p = Path(path)
+        x, y, ln = (p.with_name(p.stem + suf) for suf in ("_X.npy", "_Y.npy", "_lengths.npy"))
+        if not (x.exists() and (ln.exists() or y.exists())):
+            return None
+        out.append({"X": x, "Y": y if y.exists() else None, "lengths": ln if ln.exists() else None,
+                    "is_dynamic": ln.exists()})
+    if len({c["is_dynamic"] for c in out}) > 1:
+        raise ValueError("all memory-mapped dataset shards must use the same format")
+    return out
+
+
 def _device_int(a: np.ndarray, device) -> tuple[torch.Tensor, int]:
     """Upload an integer token array keeping a compact storage width (1/2/4/8 bytes)."""
     a = np.ascontiguousarray(a)
@@ -37,29 +97,27 @@ def _device_int(a: np.ndarray, device) -> tuple[torch.Tensor, int]:
         raise TypeError(f"token arrays must be integer, got {a.dtype}")
     if a.size == 0:
         return torch.zeros(0, dtype=torch.int32, device=device), 4
-    lo, hi = int(a.min()), int(a.max())
-    if a.dtype.itemsize == 1 and a.dtype.kind == "u":
-        eb = 1
-    elif lo >= -(1 << 15) and hi < (1 << 15) and a.dtype.itemsize <= 2:
-        eb = 2
-    elif lo >= -(1 << 31) and hi < (1 << 31) and a.dtype.itemsize <= 4:
-        eb = 4
-    else:
-        eb = 8
+    eb = _width_for(int(a.min()), int(a.max()), a.dtype)
     if eb != a.dtype.itemsize or (eb > 1 and a.dtype.kind == "u"):
         a = a.astype(_ELEM[eb])
     return torch.from_numpy(a).to(device), eb
 
 
 class DeviceCodonDataset:
-    """PackedDataset (data_loading.py:43-129) with its token store in HBM."""
+    """PackedDataset (data_loading.py:43-129) / MmapPackedDataset (:132-329, ``use_mmap``) with
+    its token store in HBM."""
 
-    def __init__(self, paths, device=None):
+    def __init__(self, paths, device=None, use_mmap: bool = False):
         if isinstance(paths, (str, os.PathLike)):
             paths = [paths]
         paths = [str(p) for p in paths]
         self.device = torch.device(device if device is not None else ("cuda", torch.cuda.current_device()))
         self.is_dynamic = False
+        self.storage_mode = "npz_memory"
+        side = _npy_sidecars(paths) if (use_mmap and paths) else None
+        if side is not None:
+            self._init_mmap(side)
+            return
         if paths:
             with np.load(paths[0], allow_pickle=False) as data:
                 self.is_dynamic = "lengths" in data
@@ -98,6 +156,47 @@ class DeviceCodonDataset:
             self.X, self._eb = _device_int(X, self.device)
             self.Y, self._ebY = _device_int(Y, self.device)
             self.n = int(X.shape[0])
+
+    def _init_mmap(self, side):
+        """Uncompressed NPY sidecars, memory-mapped (np.load(mmap_mode="r")) and streamed to HBM."""
+        self.storage_mode = "npy_mmap"
+        self.is_dynamic = side[0]["is_dynamic"]
+        if self.is_dynamic:
+            xs = [np.load(c["X"], mmap_mode="r", allow_pickle=False) for c in side]
+            lens = [np.asarray(np.load(c["lengths"], mmap_mode="r", allow_pickle=False)).astype(np.int64)
+                    for c in side]
+            self._lengths = np.concatenate(lens) if lens else np.zeros(0, np.int64)
+            starts = np.zeros(len(self._lengths), dtype=np.int64)
+            base, k = 0, 0
+            for f, ln in zip(xs, lens):
+                if len(ln):
+                    starts[k:k + len(ln)] = base + np.concatenate([[0], np.cumsum(ln[:-1])])
+                k += len(ln)
+                base += f.size
+            parts = [_device_int_stream(f.reshape(-1), self.device) for f in xs]
+            self._eb = max(eb for _, eb in parts) if parts else 4
+            nd = torch.from_numpy(np.zeros(0, _ELEM[self._eb])).dtype
+            self.flat = torch.cat([t.to(nd) for t, _ in parts]) if parts else torch.zeros(0, dtype=nd,
+                                                                                          device=self.device)
+            self.starts = torch.from_numpy(starts).to(self.device)
+            self.lens = torch.from_numpy(self._lengths).to(self.device)
+            self.n = len(self._lengths)
+            return
+        Xs = [np.load(c["X"], mmap_mode="r", allow_pickle=False) for c in side]
+        Ys = [np.load(c["Y"], mmap_mode="r", allow_pickle=False) for c in side]
+        for x, y in zip(Xs, Ys):
+            if x.shape != y.shape:
+                raise ValueError(f"X {x.shape} and Y {y.shape} must have the same shape")
+        self.T = int(Xs[0].shape[1]) if Xs and Xs[0].ndim == 2 else 0
+
+        def cat(arrs):
+            parts = [_device_int_stream(a, self.device) for a in arrs]
+            eb = max(e for _, e in parts)
+            nd = torch.from_numpy(np.zeros(0, _ELEM[eb])).dtype
+            return torch.cat([t.to(nd) for t, _ in parts]), eb
+        self.X, self._eb = cat(Xs)
+        self.Y, self._ebY = cat(Ys)
+        self.n = int(self.X.shape[0])
 
     def __len__(self):
         return self.n

@@ -381,8 +381,10 @@ def run_training(cfg: dict, args) -> None:
     ctrl = control_group(world)
 
     base_seed = int(cfg.get("seed", 1337))
-    train_ds = DeviceCodonDataset(train_paths, device)
-    val_ds = DeviceCodonDataset(val_paths, device)
+    # build_codon_lm_datasets(..., use_mmap) (data_loading.py:409): NPY sidecars memory-mapped
+    use_mmap = bool(cfg.get("use_mmap", False))
+    train_ds = DeviceCodonDataset(train_paths, device, use_mmap=use_mmap)
+    val_ds = DeviceCodonDataset(val_paths, device, use_mmap=use_mmap)
     batch_size = int(cfg["batch_size"])
 
     def train_loader_for(epoch_idx: int) -> DeviceBatchLoader:

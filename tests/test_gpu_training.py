@@ -52,6 +52,50 @@ def test_gather_windows_and_sequences(tmp_path, dtype):
         assert np.array_equal(x[i].cpu().numpy(), ex) and np.array_equal(y[i].cpu().numpy(), ey)
 
 
+@pytest.mark.parametrize("dtype", [np.int32, np.uint8, np.int16])
+def test_npy_mmap_sidecars(tmp_path, dtype, monkeypatch):
+    """use_mmap (MmapPackedDataset, data_loading.py:132-200): uncompressed <stem>_X / _Y /
+    _lengths .npy sidecars are memory-mapped and streamed to HBM (here in 1000-element pieces, so
+    chunk seams fall inside rows); the gathered batches equal the NPZ path's.  A path without
+    sidecars falls back to the NPZ, as the reference does."""
+    from codonlm_amd import data_loading as DL
+    monkeypatch.setattr(DL, "_CHUNK", 1000)
+    rng = np.random.default_rng(2)
+    X = rng.integers(0, 69, size=(70, 65)).astype(dtype)
+    Y = rng.integers(0, 69, size=(70, 65)).astype(dtype)
+    np.savez_compressed(tmp_path / "f.npz", X=X, Y=Y)
+    np.save(tmp_path / "f_X.npy", X)
+    np.save(tmp_path / "f_Y.npy", Y)
+    rows = np.array([3, 69, 0, 7, 7, 40], dtype=np.int64)
+    rd = torch.from_numpy(rows).to(DEV)
+    a = DL.DeviceCodonDataset([tmp_path / "f.npz"], DEV, use_mmap=True)
+    b = DL.DeviceCodonDataset([tmp_path / "f.npz"], DEV, use_mmap=False)
+    assert a.storage_mode == "npy_mmap" and b.storage_mode == "npz_memory" and len(a) == len(b) == 70
+    for u, v in zip(a.gather(rd, rows), b.gather(rd, rows)):
+        assert torch.equal(u, v)
+    assert np.array_equal(a.gather(rd, rows)[0].cpu().numpy(), X[rows].astype(np.int64))
+    # dynamic: flat X + lengths over two shards
+    lens = rng.integers(2, 80, size=40)
+    flat = rng.integers(1, 69, size=int(lens.sum())).astype(dtype)
+    cut = int(lens[:15].sum())
+    for name, fx, ln in (("d1", flat[:cut], lens[:15]), ("d2", flat[cut:], lens[15:])):
+        np.savez(tmp_path / f"{name}.npz", X=fx, lengths=ln)
+        np.save(tmp_path / f"{name}_X.npy", fx)
+        np.save(tmp_path / f"{name}_lengths.npy", ln)
+    paths = [tmp_path / "d1.npz", tmp_path / "d2.npz"]
+    a = DL.DeviceCodonDataset(paths, DEV, use_mmap=True)
+    b = DL.DeviceCodonDataset(paths, DEV)
+    assert a.storage_mode == "npy_mmap" and a.is_dynamic and np.array_equal(a.seq_lengths, b.seq_lengths)
+    rows = np.array([0, 14, 15, 39, 22], dtype=np.int64)
+    rd = torch.from_numpy(rows).to(DEV)
+    for u, v in zip(a.gather(rd, rows), b.gather(rd, rows)):
+        assert torch.equal(u, v)
+    # no sidecar for one shard -> the NPZ path for all (the reference's fallback)
+    (tmp_path / "d2_X.npy").unlink()
+    c = DL.DeviceCodonDataset(paths, DEV, use_mmap=True)
+    assert c.storage_mode == "npz_memory"
+
+
 def test_device_loader_matches_reference_order(tmp_path):
     from codonlm_amd.data_loading import DeviceBatchLoader, DeviceCodonDataset
     _, g = load_golden("data_order")
