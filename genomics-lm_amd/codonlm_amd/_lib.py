@@ -130,6 +130,8 @@ SIGNATURES = {
     "cg_gemm_set_pers_pp": (i32, [i32]),
     "cg_gemm_set_pers_pp2": (i32, [i32]),
     "cg_set_head_dw_defer": (i32, [i32]),
+    "cg_set_dw_order": (i32, [i32]),
+    "cg_set_dw_group": (i32, [i32]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),
     "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),

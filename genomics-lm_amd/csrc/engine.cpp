@@ -82,9 +82,11 @@ static int dw_tile_for(const Dims& D, int n, double* cost_out) {
   if (cost_out) *cost_out = best_cost;
   return best;
 }
+static int g_dw_group = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
+static int g_dw_order = [] { const char* e = getenv("CG_DW_ORDER"); return e ? atoi(e) : 1; }();
 DwPlan dw_plan(const cg_model_cfg* c, const Dims& D) {
   if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128};
-  static const int forced_g = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
+  const int forced_g = g_dw_group;
   const int gmax = std::min(D.L, CG_DW_MAX / 4);
   DwPlan best{1, 128};
   double best_cost = 1e30;
@@ -520,10 +522,14 @@ int bias_grad(const Ctx& C, const void* dy, long long lddy, int N, long long gof
 
 float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 
-// dW groups run from block L-1 downwards; the short remainder group (L mod G blocks) comes FIRST,
-// so the first blocks' gradient buckets are final -- and their data-parallel all-reduce starts --
-// after that group instead of after G blocks (C4: groups of 2, 5, 5 from the top)
-int first_group(const Dims& D) { return D.L % D.G ? D.L % D.G : D.G; }
+// dW groups run from block L-1 downwards.  Order 1 (default since round 4): the short remainder
+// group (L mod G blocks) comes LAST (C4: groups of 5, 5, 2 from the top), so the buckets whose
+// all-reduce can only start after the final dW launch are the short group's (25 MB instead of
+// 63 MB at C4).  Order 0 (cg_set_dw_order): the remainder first (2, 5, 5), so the first buckets
+// are final after 2 blocks instead of 5.  tools/bucket_replay.py priced both on one GPU with the
+// all-reduces modelled as CU-holding side-stream kernels: 5/5/2 8.22 / 8.44 ms against 2/5/5
+// 8.31 / 8.63 ms per C4 step at 600 / 300 GB/s bus bandwidth.
+int first_group(const Dims& D) { return (g_dw_order == 0 && D.L % D.G) ? D.L % D.G : D.G; }
 // position of block l inside its group, counted from the group's top block
 int slot_of(const Dims& D, int l) {
   const int u = D.L - 1 - l, f = first_group(D);
@@ -620,6 +626,16 @@ static int g_head_dw_defer = [] {
   return e ? atoi(e) : 1;
 }();
 }  // namespace
+extern "C" int cg_set_dw_order(int order) {
+  const int prev = g_dw_order;
+  g_dw_order = order ? 1 : 0;
+  return prev;
+}
+extern "C" int cg_set_dw_group(int blocks) {
+  const int prev = g_dw_group;
+  g_dw_group = blocks < 0 ? 0 : blocks;
+  return prev;
+}
 extern "C" int cg_set_head_dw_defer(int on) {
   const int prev = g_head_dw_defer;
   g_head_dw_defer = on ? 1 : 0;

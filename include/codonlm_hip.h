@@ -493,6 +493,12 @@ int cg_diag_occupy(int n_cus, int usec, void* stream);
  * into the first grouped dW launch: 1 (default; env CG_HEAD_DW_DEFER at load) or 0 (a split-K
  * product in phase 0).  Returns the previous setting. */
 int cg_set_head_dw_defer(int on);
+/* grouped dW plan controls (read when a backward starts; change them only between steps):
+ * cg_set_dw_order 1 = the short remainder group last from the top (default; env CG_DW_ORDER),
+ * 0 = first; cg_set_dw_group(n) forces n blocks per group (0 = planner's choice; env
+ * CG_DW_GROUP).  Both return the previous setting. */
+int cg_set_dw_order(int order);
+int cg_set_dw_group(int blocks);
 
 /* "codonlm_hip <abi> gfx950".  ABI 0.2 (round 3): cg_gemm_desc.ws_bytes and the size_t
  * workspace-size argument after every workspace pointer.  ABI 0.3 (round 4): cg_model gained

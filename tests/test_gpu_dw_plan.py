@@ -1,6 +1,10 @@
-"""The tied head's weight gradient, deferred from backward phase 0 into the first grouped dW
-launch (engine.cpp flush_dw): deferral on vs off, and the phase-2 fallback of a
-partial phase sequence (phase 0 then phase 2, no dW group to take the product).
+"""The grouped weight-gradient plan of the bf16 engine (engine.cpp dw_plan / flush_dw).
+
+* the tied head's weight gradient, deferred from backward phase 0 into the first grouped dW
+  launch: deferral on vs off, and the phase-2 fallback of a partial phase sequence
+  (phase 0 then phase 2, no dW group to take the product);
+* the group plans priced by tools/bucket_replay.py (short group first / last, 4/4/4, 6/6) give
+  the gradients of one block per launch, and fire every block's bucket hook exactly once.
 
 Reference: the head is tied to tok_emb (model_tiny_gpt.py:217-219), so d(tok_emb) = the head's
 dlogits^T . ln_f(x) plus the embedding scatter-add (loss.backward(), loop.py:1233).
@@ -71,3 +75,31 @@ def test_head_dw_partial_phases_runs_deferred_product():
     te_on, te_off = on["tok_emb.weight"], off["tok_emb.weight"]
     assert float(te_off.abs().max()) > 0
     assert _rel(te_on, te_off) < 1e-5
+
+
+def test_dw_group_orders_give_the_same_gradients():
+    from codonlm_amd import TinyGPT, _lib as L
+    x, y = _batch()
+
+    def run(order, group):
+        o1, o2 = L.lib.cg_set_dw_order(order), L.lib.cg_set_dw_group(group)
+        try:
+            torch.manual_seed(5)
+            m = TinyGPT(68, 128, n_layer=12, n_head=4, n_embd=128, dropout=0.0, compute_dtype="bf16", device=DEV)
+            m.train()
+            fired = []
+            m._bucket_hook = fired.append
+            _, loss = m(x, y)
+            loss.backward()
+            torch.cuda.synchronize()
+            return m.flat_grads().detach().clone(), fired
+        finally:
+            L.lib.cg_set_dw_order(o1)
+            L.lib.cg_set_dw_group(o2)
+
+    ref, fired_ref = run(0, 1)
+    assert sorted(map(str, fired_ref)) == sorted(map(str, ["head", "embed", *range(12)]))
+    for order, group in ((0, 5), (1, 5), (0, 4), (1, 6), (1, 12)):
+        g, fired = run(order, group)
+        assert sorted(map(str, fired)) == sorted(map(str, fired_ref)), (order, group, fired)
+        assert _rel(g, ref) < 1e-6, (order, group)
