@@ -21,6 +21,7 @@ CG_OK, CG_EINVAL, CG_EUNSUPPORTED, CG_ELAUNCH = 0, -1, -2, -3
 EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1, 2, 4, 8, 16, 32, 64
 EPI_SWIGLU, EPI_DSWIGLU = 128, 256
 EPI_GELU_DERIV = 512  # GELU: aux_out = gelu'(v); DGELU: aux holds gelu' (out = v * aux)
+EPI_ROPE = 1024  # rotate-half RoPE of the q / k head columns after the bias (loader-wave tile only)
 (PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV,
  PROBE_GEMM_DW_GROUPED, PROBE_GEMM_PERS) = range(9)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
@@ -54,7 +55,8 @@ class GemmDesc(C.Structure):
                 ("bias", vp), ("resid", vp), ("ldr", i64),
                 ("aux", vp), ("aux_out", vp), ("ld_aux", i64),
                 ("drop_seed", u32), ("drop_p", f32), ("split_k", i32), ("workspace", vp),
-                ("n_valid", i32), ("ws_bytes", sz)]
+                ("n_valid", i32), ("ws_bytes", sz),
+                ("rope_cos", vp), ("rope_sin", vp), ("rope_T", i32), ("rope_hd", i32), ("rope_heads", i32)]
 
 
 DW_MAX = 32
@@ -129,6 +131,7 @@ SIGNATURES = {
     "cg_gemm_set_pers_lw": (i32, [i32]),
     "cg_gemm_set_pers_pp": (i32, [i32]),
     "cg_gemm_set_pers_pp2": (i32, [i32]),
+    "cg_set_rope_fused": (i32, [i32]),
     "cg_set_head_dw_defer": (i32, [i32]),
     "cg_set_dw_order": (i32, [i32]),
     "cg_set_dw_group": (i32, [i32]),
@@ -158,6 +161,8 @@ SIGNATURES = {
     "cg_attn_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
                           u32, f32, vp, vp, i64, vp, sz, vp]),
+    "cg_attn_bwd_rope": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
+                               u32, f32, vp, vp, i64, vp, vp, vp, sz, vp]),
     "cg_ce_workspace": (sz, [i32]),
     "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, sz, vp]),
     "cg_swiglu_fwd": (i32, [i32, vp, i64, i32, vp, i64, i32, i32, vp]),

@@ -28,9 +28,11 @@ def _p(t):
 
 def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=None, out_dtype=None,
          bias=None, resid=None, epilogue=0, aux=None, aux_out=None, alpha=1.0, drop_seed=0, drop_p=0.0,
-         split_k=1, colsum_out=None, n_valid=0):
+         split_k=1, colsum_out=None, n_valid=0, rope=None):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); A(m,k)=a[m,k] if a_kcontig else a[k,m]; same for B.
-    colsum_out (fp32 [N]): also the column sums of C (CG_EPI_COLSUM partials + cg_colsum_reduce)."""
+    colsum_out (fp32 [N]): also the column sums of C (CG_EPI_COLSUM partials + cg_colsum_reduce).
+    rope = (cos, sin, T, hd, heads): CG_EPI_ROPE -- the first heads*hd columns rotated at position
+    m % T after the bias (tables fp32 [>= T][hd/2])."""
     for t in (a, b):
         L.require_device(t, "gemm")
     if a.dtype != b.dtype:
@@ -70,6 +72,11 @@ def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=No
     d.split_k, d.workspace = int(split_k), _p(ws)
     d.ws_bytes = 0 if ws is None else ws.numel() * ws.element_size()
     d.n_valid = int(n_valid)
+    if rope is not None:
+        cos, sin, rT, rhd, rheads = rope
+        d.epilogue |= L.EPI_ROPE
+        d.rope_cos, d.rope_sin = cos.data_ptr(), sin.data_ptr()
+        d.rope_T, d.rope_hd, d.rope_heads = int(rT), int(rhd), int(rheads)
     L.check(L.lib.cg_gemm(C.byref(d), L.stream_ptr(a.device)), "cg_gemm")
     if colsum_out is not None:
         L.check(L.lib.cg_colsum_reduce(ws.data_ptr(), (M + 63) // 64, N, colsum_out.data_ptr(), 0,
@@ -214,16 +221,22 @@ def attn_fwd_keep(qkv, segstart, B, T, H, KV, hd, drop_seed, drop_p, window=0, m
 
 
 def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None,
-             bias_part=None):
+             bias_part=None, rope=None):
     """dqkv; with bias_part (fp32 [B*ceil(T/128)][ld >= (H+2KV) hd], bf16 MFMA path) also the per-tile
-    column sums of dqkv that cg_colsum_reduce turns into the q/k/v bias gradients."""
+    column sums of dqkv that cg_colsum_reduce turns into the q/k/v bias gradients.  rope = (cos, sin)
+    fp32 [T][hd/2] tables: qkv holds rotated q / k and dQ / dK come back w.r.t. the un-rotated ones
+    (cg_attn_bwd_rope, bf16 MFMA path)."""
     dqkv = torch.zeros_like(qkv)
     ws = torch.empty(int(L.lib.cg_attn_bwd_workspace(B, T, H)) // 4 + 1, dtype=torch.float32, device=qkv.device)
-    L.check(L.lib.cg_attn_bwd(_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0),
-                              dy.data_ptr(), dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), B, T, H,
-                              KV, hd, int(window or 0), int(drop_seed) & 0xFFFFFFFF, float(drop_p), _p(drop_mask),
-                              _p(bias_part), 0 if bias_part is None else bias_part.stride(0),
-                              ws.data_ptr(), ws.numel() * 4, L.stream_ptr(qkv.device)), "cg_attn_bwd")
+    args = [_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0), dy.data_ptr(),
+            dy.stride(0), lse.data_ptr(), dqkv.data_ptr(), dqkv.stride(0), B, T, H, KV, hd, int(window or 0),
+            int(drop_seed) & 0xFFFFFFFF, float(drop_p), _p(drop_mask), _p(bias_part),
+            0 if bias_part is None else bias_part.stride(0)]
+    tail = [ws.data_ptr(), ws.numel() * 4, L.stream_ptr(qkv.device)]
+    if rope is None:
+        L.check(L.lib.cg_attn_bwd(*args, *tail), "cg_attn_bwd")
+    else:
+        L.check(L.lib.cg_attn_bwd_rope(*args, rope[0].data_ptr(), rope[1].data_ptr(), *tail), "cg_attn_bwd_rope")
     return dqkv
 
 

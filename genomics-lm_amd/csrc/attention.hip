@@ -405,7 +405,21 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
                            long long lddqkv, int B, int T, int H, int KV, int hd, int window, uint32_t drop_seed,
                            float drop_p, const void* drop_mask, float* bias_part, long long ld_part, void* ws,
                            size_t ws_bytes, void* stream) {
+  return cg_attn_bwd_rope(dtype, qkv, ldqkv, segstart, y, ldy, dy, lddy, lse, dqkv, lddqkv, B, T, H, KV, hd, window,
+                          drop_seed, drop_p, drop_mask, bias_part, ld_part, nullptr, nullptr, ws, ws_bytes, stream);
+}
+// cg_attn_bwd with the gradients of RoPE-rotated q / k rotated back (rope_cos / rope_sin: the
+// [>= T][hd/2] tables of cg_rope_tab; both NULL = no RoPE): the dQ and dK outputs -- and their
+// bias partials -- are w.r.t. the un-rotated q / k projections (the MFMA kernels only; the vector
+// path returns CG_EUNSUPPORTED with tables)
+extern "C" int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
+                                const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
+                                void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
+                                uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
+                                long long ld_part, const float* rope_cos, const float* rope_sin, void* ws,
+                                size_t ws_bytes, void* stream) {
   if (KV <= 0 || H % KV) return CG_EINVAL;
+  if ((rope_cos == nullptr) != (rope_sin == nullptr)) return CG_EINVAL;
   if (B > 0 && T > 0 && (!ws || ws_bytes < cg_attn_bwd_workspace(B, T, H))) return CG_EINVAL;
   if (hd <= 0 || hd > AV_HD) return CG_EUNSUPPORTED;
   if (B == 0 || T == 0) return CG_OK;
@@ -417,11 +431,14 @@ extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const in
   const long long nbt = (long long)B * H * T;
   const bool mfma = dtype == CG_BF16 && attn_mfma_supported(hd, ldqkv, lddy) && (lddqkv & 7) == 0 && (ldy & 7) == 0;
   if (bias_part && (!mfma || ld_part < (long long)(H + 2 * KV) * hd)) return CG_EUNSUPPORTED;
+  if (rope_cos && (!mfma || hd % 16 || ((uintptr_t)rope_cos & 15) || ((uintptr_t)rope_sin & 15)))
+    return CG_EUNSUPPORTED;
   if (mfma) {
     // delta = rowsum(dO o O) is computed inside the dQ kernel
     return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)y, ldy, (const bf16_t*)dy,
                                 lddy, lse, delta, (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr,
-                                dscale, scale, (const uint32_t*)drop_mask, bias_part, ld_part, s);
+                                dscale, scale, (const uint32_t*)drop_mask, bias_part, ld_part, s, rope_cos,
+                                rope_sin);
   }
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const bf16_t*)y, ldy,

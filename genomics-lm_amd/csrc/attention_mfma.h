@@ -299,6 +299,35 @@ __device__ __forceinline__ void store_blk16(bf16_t* rowp, const v16f& x, float s
   }
 }
 
+// Inverse rotate-half RoPE (model_tiny_gpt.py:9-45 applied after the q / k projections; its
+// gradient) on one row held in the two 32-dim accumulator blocks x0, x1 (element r of block b:
+// dim 32 b + acc_row(r)), for position `cs` / `sn` rows of the [T][hd/2] tables:
+//   dx_i = cos_i g_i + sin_i g_{i+h},  dx_{i+h} = cos_i g_{i+h} - sin_i g_i   (i < h = hd/2).
+// h is a multiple of 8, so a dim and its partner sit in the same lane (acc_row keeps 4 (l >> 5)).
+template <int HD>
+__device__ __forceinline__ void rope_inv_blocks(v16f& x0, v16f& x1, const float* cs, const float* sn, int hl) {
+  constexpr int h = HD / 2;
+  static_assert(h % 8 == 0 && h <= 32, "rope: head dim 16, 32, 48 or 64");
+#pragma unroll
+  for (int j = 0; j < h / 8; ++j) {
+    const float4 c4 = *(const float4*)(cs + 8 * j + 4 * hl);
+    const float4 s4 = *(const float4*)(sn + 8 * j + 4 * hl);
+    const float cc[4] = {c4.x, c4.y, c4.z, c4.w}, ss[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int r = t | (j << 2);                  // dim 8 j + t (+ 4 hl) of block 0
+      const int dp = 8 * j + t + h;                // its partner
+      const int rp = (dp & 3) | (((dp & 31) >> 3) << 2);
+      const float g = x0[r];
+      const float gp = dp < 32 ? x0[rp] : x1[rp];
+      x0[r] = fmaf(cc[t], g, ss[t] * gp);
+      const float np = fmaf(cc[t], gp, -ss[t] * g);
+      if (dp < 32) x0[rp] = np;
+      else x1[rp] = np;
+    }
+  }
+}
+
 // Column sums over the workgroup's 128 accumulator columns (4 waves x 32 lanes) of the 64 rows
 // held in two accumulator blocks x0 (rows 0..31) and x1 (32..63), for the bias-gradient partials:
 // the values go through LDS ([wave][row][33 lanes], conflict-free stores and reads), each thread
@@ -640,7 +669,9 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
                                                            long long lddq, int T, int H, int KV, int hd_rt, int window,
                                                            uint32_t seed, uint32_t thr, float dscale, float scale,
                                                            const uint32_t* __restrict__ qmask, int wpr,
-                                                           float* __restrict__ bpart, long long ldp) {
+                                                           float* __restrict__ bpart, long long ldp,
+                                                           const float* __restrict__ rcos,
+                                                           const float* __restrict__ rsin) {
   using namespace fa;
   constexpr int hd = HD;
   (void)hd_rt;
@@ -801,8 +832,14 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
     step(std::integral_constant<int, 0>{}, t);
     if (t + 1 <= t1) step(std::integral_constant<int, 1>{}, t + 1);
   }
-  // dQ = qscale * (dS/dscale . K)
+  // dQ = qscale * (dS/dscale . K); with RoPE the gradient w.r.t. the rotated q, rotated back
+  // (the inverse of the forward rotation at the query's position) before the store and the bias
+  // partials
   const float qscale = DROP ? scale * dscale : scale;
+  if (rcos) {
+    const size_t ro = (size_t)(qok ? myq : 0) * (hd / 2);
+    rope_inv_blocks<hd>(a0, a1, rcos + ro, rsin + ro, lane >> 5);
+  }
   {
     bf16_t* dr = dqkv + (rowbase + (qok ? myq : 0)) * lddq + (long long)hh * hd;
     store_blk16(dr, a0, qscale, qok, hd < 32 ? hd : 32, lane);
@@ -831,7 +868,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
                                                              int KV, int hd_rt, int window, uint32_t seed, uint32_t thr,
                                                              float dscale, float scale,
                                                              const uint32_t* __restrict__ qmask, int wpr,
-                                                             float* __restrict__ bpart, long long ldp) {
+                                                             float* __restrict__ bpart, long long ldp,
+                                                             const float* __restrict__ rcos,
+                                                             const float* __restrict__ rsin) {
   using namespace fa;
   constexpr int hd = HD;
   (void)hd_rt;
@@ -1069,6 +1108,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     if (it + 2 < total) iter(std::integral_constant<int, 2>{}, it + 2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the loop
+  if (rcos) {  // RoPE: dK w.r.t. the rotated k, rotated back at the key's position
+    const size_t ro = (size_t)(kok ? mykey : 0) * (hd / 2);
+    rope_inv_blocks<hd>(dk0, dk1, rcos + ro, rsin + ro, lane >> 5);
+  }
   {
     bf16_t* kr = dqkv + (rowbase + (kok ? mykey : 0)) * lddq + koff;
     bf16_t* vr = dqkv + (rowbase + (kok ? mykey : 0)) * lddq + voff;
@@ -1146,7 +1189,8 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
                                        long long ldy, const bf16_t* dy, long long lddy, const float* lse,
                                        float* delta, bf16_t* dqkv, long long lddq, int B, int T, int H, int KV,
                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale, float scale,
-                                       const uint32_t* dmask, float* bpart, long long ldp, hipStream_t s) {
+                                       const uint32_t* dmask, float* bpart, long long ldp, hipStream_t s,
+                                       const float* rcos = nullptr, const float* rsin = nullptr) {
   dim3 gq(B * H, cg_cdiv(T, 128));
   const int wpr = attn_drop_wpr(T);
   float* nlse2 = delta + (long long)B * H * T;  // second half of the workspace
@@ -1157,7 +1201,8 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_begin(CG_PROBE_ATTN_DQ, s);
 #define DQ(D, HDv)                                                                                             \
   hipLaunchKernelGGL((attn_bwd_dq_mfma<D, HDv>), gq, dim3(256), shq, s, qkv, ld, seg, dy, lddy, y, ldy, lse, \
-                     delta, nlse2, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
+                     delta, nlse2, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp, \
+                     rcos, rsin)
 #define DQH(D) if (hd == 64) DQ(D, 64); else if (hd == 48) DQ(D, 48); else DQ(D, 32)
   if (mode == 2) { DQH(2); } else if (mode == 1) { DQH(1); } else { DQH(0); }
 #undef DQH
@@ -1170,7 +1215,7 @@ static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   cg_probe_begin(CG_PROBE_ATTN_DKDV, s);
 #define DKDV(D, HDv)                                                                                            \
   hipLaunchKernelGGL((attn_bwd_dkdv_mfma<D, HDv>), gk, dim3(256), shk, s, qkv, ld, seg, dy, lddy, lse, delta, nlse2, dqkv, \
-                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp)
+                     lddq, T, H, KV, hd, window, seed, thr, dscale, scale, dmask, wpr, bpart, ldp, rcos, rsin)
 #define DKH(D) if (hd == 64) DKDV(D, 64); else if (hd == 48) DKDV(D, 48); else DKDV(D, 32)
   if (mode == 2) { DKH(2); } else if (mode == 1) { DKH(1); } else { DKH(0); }
 #undef DKH

@@ -193,6 +193,13 @@ static int g_fused_keep = [] {
   const char* e = getenv("CG_ATTN_FUSED_KEEP");
   return e ? atoi(e) : 1;
 }();
+// RoPE models: the rotation fused into the qkv projection's epilogue (forward) and into the
+// attention backward's dQ / dK stores (backward) -- 1 (default; env CG_ROPE_FUSED at load) -- or
+// the separate cg_rope_tab passes (0; also the fallback where a kernel does not implement it)
+static int g_rope_epi = [] {
+  const char* e = getenv("CG_ROPE_FUSED");
+  return e ? atoi(e) : 1;
+}();
 struct LayerAct {
   float *mean1, *rstd1, *mean2, *rstd2, *lse, *xmid;
   void *h1, *qkv, *y, *h2, *a, *g, *gu, *s;
@@ -636,6 +643,11 @@ extern "C" int cg_set_dw_group(int blocks) {
   g_dw_group = blocks < 0 ? 0 : blocks;
   return prev;
 }
+extern "C" int cg_set_rope_fused(int on) {
+  const int old = g_rope_epi;
+  g_rope_epi = on != 0;
+  return old;
+}
 extern "C" int cg_set_head_dw_defer(int on) {
   const int prev = g_head_dw_defer;
   g_head_dw_defer = on ? 1 : 0;
@@ -934,8 +946,20 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     CK(cg_layernorm_fwd(C.dt, xl, d, P(C, o.ln1w), P(C, o.ln1b), a.h1, d, a.mean1, a.rstd1, (int)M, d, eps, C.s));
     cg_gemm_desc g = lin_fwd(C, a.h1, d, o.wqkv, d, D.Nqkv, d, a.qkv, D.Nqkv);
     g.epilogue = CG_EPI_BIAS; g.bias = P(C, o.bqkv);
-    CK(cg_gemm(&g, C.s));
-    if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
+    // RoPE in the projection's epilogue where the GEMM tile implements it, else a table pass
+    int rc_rope = CG_EUNSUPPORTED;
+    if (D.rope && g_rope_epi) {
+      cg_gemm_desc gr = g;
+      gr.epilogue |= CG_EPI_ROPE;
+      gr.rope_cos = m->rope_cos; gr.rope_sin = m->rope_sin;
+      gr.rope_T = T; gr.rope_hd = D.hd; gr.rope_heads = D.H + D.KV;
+      rc_rope = cg_gemm(&gr, C.s);
+      if (rc_rope != CG_OK && rc_rope != CG_EUNSUPPORTED) return rc_rope;
+    }
+    if (rc_rope != CG_OK) {
+      CK(cg_gemm(&g, C.s));
+      if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
+    }
     const void* dmask = p > 0.f ? a.dmask : nullptr;
     if (dmask && g_fused_keep) {
       CK(cg_attn_fwd_keep(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV,
@@ -1136,22 +1160,27 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     cg_gemm_desc g = lin_dx(C, sl.gattn, d, o.wp, d, d, d, A.dsmall, d, a.pT);
     CK(cg_gemm(&g, C.s));
     // the qkv bias gradient = column sums of the (un-rotated) dqkv: produced by the MFMA attention
-    // backward itself as per-tile partials when no RoPE rotation follows, else a colsum pass
+    // backward itself as per-tile partials (with RoPE it rotates dQ / dK back before the stores and
+    // the partials), else a colsum pass after the vector kernels and the table inverse rotation
     const void* segp = m->cfg.sep_id >= 0 ? A.seg : nullptr;
     const void* dmask_b = p > 0.f ? a.dmask : nullptr;
+    const bool rope_in = D.rope && g_rope_epi;  // the inverse rotation inside the kernels
+    const float* rc_cos = rope_in ? m->rope_cos : nullptr;
+    const float* rc_sin = rope_in ? m->rope_sin : nullptr;
     int rc = CG_EUNSUPPORTED;
-    if (!D.rope)
-      rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
-                       C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, sl.bpart, D.Nqkv,
-                       A.delta, A.nb.delta, C.s);
+    if (!D.rope || rope_in)
+      rc = cg_attn_bwd_rope(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv,
+                            C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, sl.bpart,
+                            D.Nqkv, rc_cos, rc_sin, A.delta, A.nb.delta, C.s);
     const bool fused_bias = rc == CG_OK;
-    if (rc == CG_EUNSUPPORTED)
+    if (rc == CG_EUNSUPPORTED) {
       rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
                        C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, nullptr, 0,
                        A.delta, A.nb.delta, C.s);
+      if (rc == CG_OK && D.rope)
+        rc = cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s);
+    }
     CK(rc);
-    if (D.rope)
-      CK(cg_rope_tab(C.dt, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 1, C.s));
     if (fused_bias)
       CK(defer_reduce(m, sl.bpart, D.Nqkv, C.B * ((C.T + 127) / 128), D.Nqkv, G(C, o.bqkv), accumulate, C.s));
     else

@@ -26,6 +26,10 @@ struct GemmParams {
   uint32_t drop_seed, drop_thr; float drop_scale;
   float* ws; int split;
   int n_valid;  // SWIGLU / DSWIGLU live columns
+  // CG_EPI_ROPE: tables, sequence length, half head dim, 16-column pair units per head (G) and
+  // its reciprocal (U / G = (U * rope_mul) >> 16), pair units of the rotated q / k columns
+  const float* rope_cos; const float* rope_sin;
+  int rope_T, rope_half, rope_G, rope_mul, rope_uqk;
 };
 
 // ---------------------------------------------------------------------------
@@ -649,12 +653,14 @@ extern "C" int cg_gemm_set_pers_pp(int mode) {
   return old;
 }
 static bool pers_pp_for(int e) {
+  if (e & CG_EPI_ROPE) return false;
   if (g_pers_pp == 2) return true;
   return g_pers_pp == 1 && (e == 0 || e == CG_EPI_BIAS);
 }
 // the SwiGLU backward's epilogue does not fit the loader-wave kernel's 168-register budget
 static bool pers_lw_for(int e) {
   if (pers_pp_for(e)) return false;
+  if (e & CG_EPI_ROPE) return g_pers_lw != 0;  // the RoPE epilogue is the loader-wave kernel's only
   if (g_pers_lw == 2) return e != CG_EPI_DSWIGLU;
   return g_pers_lw == 1 && (e == 0 || e == CG_EPI_BIAS);
 }
@@ -686,6 +692,12 @@ static gemm_kernel_t pick_pp2(int e, int ct) {
   return nullptr;
 }
 static gemm_kernel_t pick_pers(int e, int ct) {
+  if (e & CG_EPI_ROPE) {
+    if (ct != CG_BF16 || !pers_lw_for(e)) return nullptr;
+    if (e == (CG_EPI_BIAS | CG_EPI_ROPE)) return gemm_bf16_lw_kernel<CG_EPI_BIAS | CG_EPI_ROPE, CG_BF16>;
+    if (e == CG_EPI_ROPE) return gemm_bf16_lw_kernel<CG_EPI_ROPE, CG_BF16>;
+    return nullptr;
+  }
 #define PSPEC(E, T)                                                                              \
   if (e == (E) && ct == (T))                                                                    \
     return pers_pp_for(e) ? gemm_bf16_pp_kernel<(E), (T)>                                       \
@@ -836,6 +848,24 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     if (p.epi == CG_EPI_SWIGLU ? !p.aux_out : !p.aux) return CG_EINVAL;
     p.n_valid = d->n_valid > 0 ? std::min(d->n_valid, p.N) : p.N;
   }
+  // RoPE epilogue: only the loader-wave persistent tile implements it (the caller keeps the
+  // separate cg_rope_tab pass on CG_EUNSUPPORTED)
+  const bool rope = (p.epi & CG_EPI_ROPE) != 0;
+  if (rope) {
+    if ((p.epi & ~(CG_EPI_ROPE | CG_EPI_BIAS)) || !d->rope_cos || !d->rope_sin || d->rope_T <= 0) return CG_EINVAL;
+    const int hd = d->rope_hd;
+    if (d->in_dtype != CG_BF16 || p.c_dtype != CG_BF16 || d->split_k > 1 || hd <= 0 || hd % 16 ||
+        d->rope_heads <= 0 || (long long)d->rope_heads * hd > p.N || p.N % 16 || p.N >= 65536 ||
+        (((uintptr_t)d->rope_cos | (uintptr_t)d->rope_sin) & 15))
+      return CG_EUNSUPPORTED;
+    p.rope_cos = d->rope_cos;
+    p.rope_sin = d->rope_sin;
+    p.rope_T = d->rope_T;
+    p.rope_half = hd / 2;
+    p.rope_G = hd / 16;
+    p.rope_mul = (65536 + p.rope_G - 1) / p.rope_G;
+    p.rope_uqk = d->rope_heads * hd / 16;
+  }
   int split = d->split_k > 1 ? d->split_k : 1;
   const int bkt = d->in_dtype == CG_BF16 ? bfg::BKT : 16;
   if (d->K == 0) split = 1;
@@ -870,7 +900,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     vec = vec_ok(d, split);
     gemm_kernel_t k;
     const bool pers = vec && use_pers(d, split);
-    if (swg && !pers) return CG_EUNSUPPORTED;
+    if ((swg || rope) && !pers) return CG_EUNSUPPORTED;
     if (!pers) p.epi &= ~CG_EPI_COLSUM;  // only the persistent tile fuses the column sums
     const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
     // 256x256 tiles: the products with N >= 1024 (at M = B.T >= 4096 at least one round of

@@ -21,6 +21,11 @@
 // source) are loaded two k-steps before the tile's end (or partly after its MFMAs where the
 // registers do not allow it) and waited for with vmcnt(0) -- no counted interleaving with the
 // DMA stream.
+// timing-only diagnostic builds of the RoPE epilogue (results invalid), bit set: 1 no table loads,
+// 2 B rows in natural order, 4 no rotation arithmetic, 8 C stores at the natural column positions
+#ifndef CG_ROPE_DIAG
+#define CG_ROPE_DIAG 0
+#endif
 namespace bfl {
 constexpr int CWAVES = 8, LWAVES = 4, THREADS = 64 * (CWAVES + LWAVES);
 constexpr int A_PIECES = bfw::A_BYTES / 1024, B_PIECES = bfw::B_BYTES / 1024;  // 32, 16 per stage
@@ -32,8 +37,21 @@ template <int EPI, int CT>
 __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParams p) {
   using namespace bfp;
   constexpr bool SWG = Epi<EPI, CT>::SWG, DSW = Epi<EPI, CT>::DSW;
+  constexpr bool RP = (EPI & CG_EPI_ROPE) != 0;
   constexpr int BNO = SWG ? BN / 2 : BN;
   constexpr int ES = CT == CG_BF16 ? 2 : 4;
+  // RoPE column order: logical column n = 64 w + 32 c + 8 g + e (the lane's chunk c of group g in
+  // 64-column block w) is pair unit U = 4 w + g, half c -- U < rope_uqk: head U / G, dims
+  // 8 (U % G) + e (c = 0) and their rotation partners + half (c = 1); past the q / k heads:
+  // column 16 U + 8 c + e.  Both halves of a rotation pair then sit in one lane's two chunks.
+  auto rope_col = [&](int n) __attribute__((always_inline)) {
+    const int U = ((n >> 6) << 2) | ((n >> 3) & 3), c = (n >> 5) & 1, e = n & 7;
+    if (U < p.rope_uqk) {
+      const int h = (U * p.rope_mul) >> 16;
+      return h * 2 * p.rope_half + 8 * (U - h * p.rope_G) + c * p.rope_half + e;
+    }
+    return 16 * U + 8 * c + e;
+  };
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -63,6 +81,21 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
       const int pos = (L + bfl::LWAVES * j) * 1024 + 16 * lane;
       vb[j] = SWG ? b_src_off_swg(pos, p.ldb, p.N) : b_src_off(pos, p.ldb);
     }
+    // RoPE: the B rows of a tile are not an affine image of n0 (rotation-pair order), so the
+    // loader keeps the piece offsets of the tile it is streaming (vcur) and forms the next tile's
+    // (vnext) right after issuing the last stage of the current one -- off the path between a
+    // barrier and the DMAs behind it
+    uint32_t vcur[bfl::LB], vnext[bfl::LB];
+    auto rope_offsets = [&](int k) __attribute__((always_inline)) {
+      int m0, n0;
+      tile_org(k < my_tiles ? k : 0, m0, n0);
+#pragma unroll
+      for (int j = 0; j < bfl::LB; ++j) {
+        const int pos = (L + bfl::LWAVES * j) * 1024 + 16 * lane;
+        const int row = pos >> 7, phys = (pos >> 4) & 7;
+        vnext[j] = ((uint32_t)((CG_ROPE_DIAG & 2) ? n0 + row : rope_col(n0 + row)) * (uint32_t)p.ldb + 8u * (uint32_t)(phys ^ fb(row))) * 2u;
+      }
+    };
     // stage g: the DMA origins of its (tile, k-step); past the CU's last stage every piece reads
     // out of range (zero fill into a slot nobody reads), so every step issues the same count
     auto issue = [&](int g) __attribute__((always_inline)) {
@@ -72,14 +105,27 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
         int m0, n0;
         tile_org(k, m0, n0);
         ao = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
-        bo = (uint32_t)(((long long)n0 * p.ldb + t * BKT) * 2);
+        if constexpr (RP) {
+          bo = (uint32_t)(t * BKT * 2);
+          if (t == 0) {
+#pragma unroll
+            for (int j = 0; j < bfl::LB; ++j) vcur[j] = vnext[j];
+          }
+        } else {
+          bo = (uint32_t)(((long long)n0 * p.ldb + t * BKT) * 2);
+        }
       }
       char* st = smem + (g % STAGES) * STAGE_BYTES;
 #pragma unroll
       for (int j = 0; j < bfl::LA; ++j) bfw::dma16(ra, st + (L + bfl::LWAVES * j) * 1024, ao + va[j]);
 #pragma unroll
-      for (int j = 0; j < bfl::LB; ++j) bfw::dma16(rb, st + A_BYTES + (L + bfl::LWAVES * j) * 1024, bo + vb[j]);
+      for (int j = 0; j < bfl::LB; ++j)
+        bfw::dma16(rb, st + A_BYTES + (L + bfl::LWAVES * j) * 1024, RP ? (bo == OOR ? OOR : bo + vcur[j]) : bo + vb[j]);
+      if constexpr (RP) {
+        if ((g + 1) % nt == 0) rope_offsets((g + 1) / nt);
+      }
     };
+    if constexpr (RP) rope_offsets(0);
     issue(0);
     issue(1);
     for (int g = 0; g < S; ++g) {
@@ -98,6 +144,7 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
   u32x4 xa[4][2], xb[4][2], bq[2][2];
   // the lane's columns of tile k (chunks c = 0, 1) and its C offsets (OOR outside the matrix)
   auto cols_of = [&](int n0, int c) __attribute__((always_inline)) {
+    if constexpr (RP) return rope_col(n0 + wn + 32 * c + 8 * g4);
     return SWG ? n0 + (wn >> 1) + 8 * g4 : n0 + wn + 32 * c + 8 * g4;
   };
   // epilogue operand loads of tile k for the lane's row groups [LO, HI) (+ the bias with BIAS_);
@@ -208,7 +255,9 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
       const int row = m0 + wm + 16 * i + r16;
 #pragma unroll
       for (int c = 0; c < 2; ++c)
-        off_c[i][c] = (row < p.M && col[c] < p.N) ? (uint32_t)(((long long)row * p.ldc + col[c]) * ES) : OOR;
+        off_c[i][c] = (row < p.M && col[c] < p.N)
+                          ? (uint32_t)(((long long)row * p.ldc + ((RP && (CG_ROPE_DIAG & 8)) ? n0 + wn + 32 * c + 8 * g4 : col[c])) * ES)
+                          : OOR;
     }
     float bia[2][8];
     if constexpr ((EPI & CG_EPI_BIAS) != 0) {
@@ -268,6 +317,62 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
           bst(rc, off_c[i][c], pack_bf16(dg));
           bst(rc, off_c[i][c] == OOR ? OOR : off_c[i][c] + (uint32_t)p.N * 2u, pack_bf16(du));
         }
+      }
+      return;
+    } else if constexpr (RP) {
+      // chunk 0 = dims i, chunk 1 = dims i + half of one q / k head (a V pair unit: cos 1, sin 0
+      // from out-of-range table loads): y_i = x_i cos - x_{i+h} sin, y_{i+h} = x_{i+h} cos + x_i sin
+      // at the row's position m % rope_T (model_tiny_gpt.py:35-45)
+      const int U = (((n0 + wn) >> 6) << 2) | g4;
+      const bool rot = U < p.rope_uqk;
+      const int dim0 = rot ? 8 * (U - ((U * p.rope_mul) >> 16) * p.rope_G) : 0;
+      const long long tab_bytes = (long long)p.rope_T * p.rope_half * 4;
+      const __amdgpu_buffer_rsrc_t rcs = rsrc(p.rope_cos, tab_bytes), rsn = rsrc(p.rope_sin, tab_bytes);
+      u32x4 cq[4][2], sq[4][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm + 16 * i + r16;
+        const uint32_t t = (uint32_t)row % (uint32_t)p.rope_T;
+        const uint32_t o = rot ? (t * (uint32_t)p.rope_half + (uint32_t)dim0) * 4u : OOR;
+        if (CG_ROPE_DIAG & 1) {
+          cq[i][0] = cq[i][1] = sq[i][0] = sq[i][1] = (u32x4){o, o, o, o};
+        } else {
+          cq[i][0] = bld(rcs, o);
+          cq[i][1] = bld(rcs, o + 16);
+          sq[i][0] = bld(rsn, o);
+          sq[i][1] = bld(rsn, o + 16);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v0[8], v1[8], cs[8], sn[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v0[4 * h + u] = acc[i][h][u];
+            v1[4 * h + u] = acc[i][2 + h][u];
+          }
+        if constexpr ((EPI & CG_EPI_BIAS) != 0) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            v0[j] += bia[0][j];
+            v1[j] += bia[1][j];
+          }
+        }
+        unpack_f32(cq[i][0], cq[i][1], cs);
+        unpack_f32(sq[i][0], sq[i][1], sn);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if (CG_ROPE_DIAG & 4) continue;
+          const float c = rot ? cs[j] : 1.0f;
+          const float y0 = fmaf(v0[j], c, -v1[j] * sn[j]);
+          const float y1 = fmaf(v1[j], c, v0[j] * sn[j]);
+          v0[j] = y0;
+          v1[j] = y1;
+        }
+        bst(rc, off_c[i][0], pack_bf16(v0));
+        bst(rc, off_c[i][1], pack_bf16(v1));
       }
       return;
     }

@@ -41,9 +41,15 @@ enum {
                          /* pre-activations g|u, C [M][N] = silu(g) * u (0 for n >= n_valid) */
   CG_EPI_DSWIGLU = 256,  /* v = dL/ds; aux = g|u [M][2N]: C [M][2N] = d(g|u)             */
                          /* (0 for n >= n_valid)                                         */
-  CG_EPI_GELU_DERIV = 512 /* modifies GELU / DGELU: the forward's aux_out receives gelu'(v) */
+  CG_EPI_GELU_DERIV = 512, /* modifies GELU / DGELU: the forward's aux_out receives gelu'(v) */
                          /* instead of v, and the backward's aux holds gelu' (out = v*aux): */
                          /* the derivative is formed once, from the unrounded pre-activation */
+  CG_EPI_ROPE = 1024     /* (with or without BIAS) rotate-half RoPE of the q / k heads after */
+                         /* the bias (model_tiny_gpt.py:91-93): columns [0, rope_heads*rope_hd) */
+                         /* of row m rotated at position m % rope_T by the rope_cos / rope_sin */
+                         /* [>= rope_T][rope_hd/2] tables (16-B aligned); bf16 in / out, the */
+                         /* loader-wave persistent tile only (else CG_EUNSUPPORTED); rope_hd */
+                         /* % 16 == 0 and N % 16 == 0                                   */
 };
 
 /*
@@ -71,6 +77,9 @@ typedef struct {
   int split_k; float* workspace;
   int n_valid; /* SWIGLU / DSWIGLU: columns < n_valid are live (0 = all N) */
   size_t ws_bytes; /* bytes at `workspace` */
+  /* CG_EPI_ROPE (ABI 0.3): tables and geometry */
+  const float* rope_cos; const float* rope_sin;
+  int rope_T, rope_hd, rope_heads;
 } cg_gemm_desc;
 int cg_gemm(const cg_gemm_desc* d, void* stream);
 /* bf16 tile selection: -1 auto (default; env CG_GEMM_WIDE overrides at load), 0 = 128x128
@@ -232,6 +241,18 @@ int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
                 void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
                 uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
                 long long ld_part, void* ws, size_t ws_bytes, void* stream);
+/* cg_attn_bwd for RoPE models (ABI 0.3): qkv holds the ROTATED q / k (model_tiny_gpt.py:91-93
+ * applies RotaryEmbedding after the projection), and the dQ / dK outputs -- and bias_part -- are
+ * rotated back to the gradients w.r.t. the un-rotated projections in the kernels' registers
+ * (the inverse rotation at each row's position), replacing a separate inverse-rotation pass.
+ * rope_cos / rope_sin: 16-B aligned fp32 [>= T][hd/2] tables as cg_rope_tab takes; both NULL =
+ * cg_attn_bwd.  Tables with a non-MFMA configuration (fp32, hd not 32/48/64): CG_EUNSUPPORTED. */
+int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
+                     const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
+                     void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
+                     uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
+                     long long ld_part, const float* rope_cos, const float* rope_sin, void* ws,
+                     size_t ws_bytes, void* stream);
 
 /* Label-smoothed, class-weighted, ignore_index cross-entropy fwd+bwd over logits rows
  * (F.cross_entropy at model_tiny_gpt.py:343-349).  logits fp32 [rows][ldl], V used
@@ -493,6 +514,10 @@ int cg_diag_occupy(int n_cus, int usec, void* stream);
  * into the first grouped dW launch: 1 (default; env CG_HEAD_DW_DEFER at load) or 0 (a split-K
  * product in phase 0).  Returns the previous setting. */
 int cg_set_head_dw_defer(int on);
+/* RoPE models: 1 (default; env CG_ROPE_FUSED at load) rotates inside the qkv projection's GEMM
+ * epilogue (CG_EPI_ROPE) and the attention backward (cg_attn_bwd_rope), 0 uses the separate
+ * cg_rope_tab passes.  Returns the previous setting. */
+int cg_set_rope_fused(int on);
 /* grouped dW plan controls (read when a backward starts; change them only between steps):
  * cg_set_dw_order 1 = the short remainder group last from the top (default; env CG_DW_ORDER),
  * 0 = first; cg_set_dw_group(n) forces n blocks per group (0 = planner's choice; env

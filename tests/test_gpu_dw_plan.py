@@ -103,3 +103,35 @@ def test_dw_group_orders_give_the_same_gradients():
         g, fired = run(order, group)
         assert sorted(map(str, fired)) == sorted(map(str, fired_ref)), (order, group, fired)
         assert _rel(g, ref) < 1e-6, (order, group)
+
+
+@pytest.mark.parametrize("hd,dropout", [(48, 0.0), (64, 0.1), (32, 0.1)])
+def test_rope_fused_equals_table_passes(hd, dropout):
+    """RoPE models (model_tiny_gpt.py:91-93): the rotation fused into the qkv projection's GEMM
+    epilogue and the attention backward's dQ / dK stores (cg_set_rope_fused(1), the default)
+    against the separate cg_rope_tab passes (0).  The fused forward rounds q / k to bf16 once
+    instead of twice, so loss within 2e-3 relative and every gradient within rel-L2 3e-2 (the
+    bf16 step's own noise between two roundings of the same values)."""
+    from codonlm_amd import TinyGPT, _lib as L
+
+    def run(fused):
+        old = L.lib.cg_set_rope_fused(int(fused))
+        try:
+            torch.manual_seed(11)
+            m = TinyGPT(68, 256, n_layer=2, n_head=4, n_kv_head=2, n_embd=4 * hd, dropout=dropout,
+                        label_smoothing=0.05, use_rope=True, use_swiglu=True, compute_dtype="bf16", device=DEV)
+            m.train()
+            x, y = _batch(B=4, T=256, seed=5)
+            m.flat_grads().zero_()
+            _, loss = m(x, y)
+            loss.backward()
+            torch.cuda.synchronize()
+            return float(loss), {k: v.grad.detach().clone() for k, v in m.named_parameters() if v.grad is not None}
+        finally:
+            L.lib.cg_set_rope_fused(old)
+    lf, gf = run(True)
+    lu, gu = run(False)
+    assert abs(lf - lu) <= 2e-3 * abs(lu), (lf, lu)
+    assert gf.keys() == gu.keys()
+    for k in gf:
+        assert _rel(gf[k], gu[k]) < 3e-2, (k, _rel(gf[k], gu[k]))

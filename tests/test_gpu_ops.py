@@ -426,6 +426,77 @@ def test_attention_bwd_bias_partials(B, T, H, KV, hd, p):
     assert float((got - ref).abs().max() / ref.abs().max()) <= 2e-3
 
 
+def _rope_tabs(T, hd):
+    half = hd // 2
+    inv = 1.0 / (10000 ** (torch.arange(half, dtype=torch.float64) / half))
+    ang = torch.arange(T, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.cos(ang).float(), torch.sin(ang).float()
+
+
+def _rope_ref(x, cos, sin, nh, hd):
+    """rotate-half RoPE (model_tiny_gpt.py:35-45) on nh heads of x [B*T][nh*hd] (T = cos rows)."""
+    T, half = cos.shape
+    xv = x.view(-1, T, nh, hd)
+    a, b = xv[..., :half], xv[..., half:]
+    c, s = cos[None, :, None, :], sin[None, :, None, :]
+    return torch.cat([a * c - b * s, b * c + a * s], -1).reshape(x.shape)
+
+
+@pytest.mark.parametrize("B,T,H,KV,hd,p", [(2, 1024, 8, 8, 64, 0.1), (2, 512, 8, 4, 48, 0.0),
+                                             (2, 300, 8, 4, 48, 0.1), (1, 130, 4, 2, 32, 0.0)])
+def test_attention_bwd_rope_fused(B, T, H, KV, hd, p):
+    """cg_attn_bwd_rope: the inverse RoPE rotation of dQ / dK inside the MFMA backward kernels
+    (model_tiny_gpt.py:91-93 rotates q, k after the projection; the engine's RoPE backward since
+    round 4) against fp32 autograd through rotation + attention of the same bf16-rounded
+    projections (rel-L2 <= 2e-2 per q / k / v block, as the plain MFMA backward), against the
+    unfused path (backward, then the cg_rope_tab inverse pass; the fused one rounds once instead
+    of twice: rel <= 1e-2), and its bias partials against the column sums of its own dqkv."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(T + hd + 1)
+    N = (H + 2 * KV) * hd
+    proj = _bf(torch.randn(B * T, N, generator=g))
+    idx = torch.randint(4, 68, (B, T), generator=g)
+    idx[0, T // 2] = 3
+    cos, sin = _rope_tabs(T, hd)
+    pr = proj.clone().requires_grad_(True)
+    q = _rope_ref(pr[:, :H * hd], cos, sin, H, hd)
+    k = _rope_ref(pr[:, H * hd:(H + KV) * hd], cos, sin, KV, hd)
+    rot = torch.cat([q, k, pr[:, (H + KV) * hd:]], 1)
+    seed = 4242
+    drop = None
+    if p > 0:
+        keep = O.dropout_keep(seed, np.arange(B * H * T)[:, None], np.arange(T)[None, :], p)
+        drop = torch.from_numpy(keep.astype(np.float32) / (1 - p)).view(B, H, T, T)
+    ref = _attn_ref(rot, idx, B, T, H, KV, hd, 3, None, drop)
+    dy = _bf(torch.randn(B * T, H * hd, generator=g))
+    ref.backward(dy)
+    seg = ops.segment_starts(idx.to(DEV), 3)
+    cd, sd = cos.to(DEV), sin.to(DEV)
+    qkv = proj.to(DEV, torch.bfloat16)
+    ops.rope_(qkv, B, T, H, KV, hd, cd, sd)
+    y, lse = ops.attn_fwd(qkv, seg, B, T, H, KV, hd, drop_seed=seed, drop_p=p)
+    dyd = dy.to(DEV, torch.bfloat16)
+    nrb = B * ((T + 127) // 128)
+    part = torch.full((nrb, N), float("nan"), device=DEV)
+    fused = ops.attn_bwd(qkv, seg, y, dyd, lse, B, T, H, KV, hd, drop_seed=seed, drop_p=p, bias_part=part,
+                         rope=(cd, sd))
+    unf = ops.attn_bwd(qkv, seg, y, dyd, lse, B, T, H, KV, hd, drop_seed=seed, drop_p=p)
+    ops.rope_(unf, B, T, H, KV, hd, cd, sd, inverse=True)
+    ff, uf = fused.float().cpu(), unf.float().cpu()
+
+    def rel(a, b):
+        return float((a.double() - b.double()).norm() / b.double().norm())
+    for name, sl in (("dq", slice(0, H * hd)), ("dk", slice(H * hd, (H + KV) * hd)),
+                     ("dv", slice((H + KV) * hd, N))):
+        assert rel(ff[:, sl], pr.grad[:, sl]) <= 2e-2, (name, rel(ff[:, sl], pr.grad[:, sl]))
+        assert rel(ff[:, sl], uf[:, sl]) <= 1e-2, (name, rel(ff[:, sl], uf[:, sl]))
+    assert torch.equal(ff[:, (H + KV) * hd:], uf[:, (H + KV) * hd:])  # dV: same kernel, no rotation
+    got = part.sum(0)
+    colsum = fused.float().sum(0)
+    assert torch.isfinite(got).all()
+    assert float((got - colsum).abs().max() / colsum.abs().max()) <= 2e-3
+
+
 def _mask_bits(words, T):
     """Unpack attn_drop_mask words -- tile-major [BH, nt, T, 2] (nt = ceil(T/64) key tiles), pair-split
     bit order -- into bool [BH, T(query), T(key)]."""
@@ -830,3 +901,77 @@ def test_gemm_colsum_epilogue(dtype, pers):
     tol = 1e-3 if dtype == torch.float32 else 2e-2
     assert (y.float().cpu() - base).abs().max() < tol * 4 * (1 + base.abs().max())
     assert (cs.cpu() - base.sum(0)).abs().max() < tol * (1 + base.abs().sum(0).max())
+
+
+@pytest.mark.parametrize("cap", [1, 3])
+@pytest.mark.parametrize("M,K,T,H,KV,hd,extra", [(16384, 384, 512, 8, 4, 48, 0), (700, 128, 77, 4, 2, 32, 0),
+                                                 (513, 256, 513, 2, 1, 64, 64), (300, 128, 100, 1, 1, 48, 0),
+                                                 (2048, 512, 1024, 8, 8, 64, 0)])
+def test_gemm_rope_epilogue(cap, M, K, T, H, KV, hd, extra):
+    """CG_EPI_ROPE (the qkv projection with RoPE fused into the loader-wave tile's epilogue,
+    model_tiny_gpt.py:85-93): B rows fed in rotation-pair order so each lane holds dims i and
+    i + hd/2 of one head, rotated after the bias at position m % T.  Against fp32 torch of the same
+    bf16 operands (rel-L2 <= 4e-3: one bf16 rounding), against the bias-only GEMM + cg_rope_tab pass
+    (<= 1e-2: that one rounds twice), and the V columns (and `extra` columns past them) against the
+    bias-only GEMM (unrotated: within one bf16 ulp).  Shapes: C3 (hd48, N 768), hd32, hd64 with
+    N % 64 != 0 rows of pair units, one head pair with N = 144 (a 64-column block half past N), C4
+    geometry; cap = 3 workgroups each walk many tiles (the per-tile B-row order)."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    g = torch.Generator().manual_seed(M + hd + extra)
+    N = (H + 2 * KV) * hd + extra
+    x = _bf(torch.randn(M, K, generator=g))
+    w = _bf(torch.randn(N, K, generator=g) * K ** -0.5)
+    bias = torch.randn(N, generator=g)
+    cos, sin = _rope_tabs(T, hd)
+    ref = x @ w.t() + bias
+    nq = (H + KV) * hd
+    pos = torch.arange(M) % T
+    rh = ref[:, :nq].view(M, H + KV, hd)
+    a, b = rh[..., :hd // 2], rh[..., hd // 2:]
+    c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+    ref_rot = torch.cat([torch.cat([a * c - b * s, b * c + a * s], -1).reshape(M, nq), ref[:, nq:]], 1)
+    xd, wd, bd = x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16), bias.to(DEV)
+    cd, sd = cos.to(DEV), sin.to(DEV)
+    old = L.lib.cg_gemm_set_pers(cap)
+    try:
+        fused = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bd, epilogue=L.EPI_BIAS, rope=(cd, sd, T, hd, H + KV))
+        plain = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bd, epilogue=L.EPI_BIAS)
+        unf = plain.clone()
+        if M % T == 0:
+            ops.rope_(unf, M // T, T, H, KV, hd, cd, sd)
+        torch.cuda.synchronize()
+    finally:
+        L.lib.cg_gemm_set_pers(old)
+    ff = fused.float().cpu()
+
+    def rel(u, v):
+        return float((u.double() - v.double()).norm() / v.double().norm())
+    assert rel(ff, ref_rot) <= 4e-3, rel(ff, ref_rot)
+    assert rel(ff[:, :nq], ref_rot[:, :nq]) <= 4e-3
+    if M % T == 0:
+        assert rel(ff, unf.float().cpu()) <= 1e-2
+    pv = plain.float().cpu()[:, nq:]
+    assert torch.allclose(ff[:, nq:], pv, rtol=2 ** -7, atol=1e-6), (ff[:, nq:] - pv).abs().max()
+
+
+def test_gemm_rope_epilogue_unsupported():
+    """CG_EPI_ROPE outside the loader-wave tile is CG_EUNSUPPORTED (the engine then keeps the
+    cg_rope_tab pass): fp32 operands, hd % 16 != 0, loader waves off."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    cos, sin = _rope_tabs(64, 40)
+    x = torch.randn(256, 128, device=DEV)
+    w = torch.randn(3 * 40 * 4, 128, device=DEV)
+    with pytest.raises(ValueError, match="CG_EUNSUPPORTED"):
+        ops.gemm(x, w, rope=(cos.to(DEV), sin.to(DEV), 64, 40, 8))
+    xb, wb = x.bfloat16(), w.bfloat16()
+    with pytest.raises(ValueError, match="CG_EUNSUPPORTED"):
+        ops.gemm(xb, wb, rope=(cos.to(DEV), sin.to(DEV), 64, 40, 8))
+    c2, s2 = _rope_tabs(64, 32)
+    old = L.lib.cg_gemm_set_pers_lw(0)
+    try:
+        with pytest.raises(ValueError, match="CG_EUNSUPPORTED"):
+            ops.gemm(xb, wb[:256], rope=(c2.to(DEV), s2.to(DEV), 64, 32, 4))
+    finally:
+        L.lib.cg_gemm_set_pers_lw(old)
