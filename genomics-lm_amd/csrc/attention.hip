@@ -448,6 +448,11 @@ extern "C" int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, con
                        (const float*)dy, lddy, delta, B, T, H, hd);
   }
   CG_LAUNCH_CHECK();
+  // fp32: the f32-MFMA kernels (exact fp32 products) where the layout allows
+  if (dtype != CG_BF16 && attn_f32mfma_supported(hd, qkv, ldqkv, dy, lddy) && (lddqkv & 3) == 0 &&
+      ((uintptr_t)dqkv & 15) == 0)
+    return attn_bwd_f32mfma_launch((const float*)qkv, ldqkv, segstart, (const float*)dy, lddy, lse, delta,
+                                   (float*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr, dscale, scale, s);
   dim3 gq(cg_cdiv(T, AV_TQ), B * H), gk(cg_cdiv(T, AV_TQ), B * KV);
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_bwd_dq_vec<bf16_t>, gq, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart,
