@@ -160,20 +160,54 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
-// fp32 kernel for K-contiguous operands (the parity-mode forward and every product whose
-// operands are row-major in K): 128x128x16 tile, 4 waves of 64x64, v_mfma_f32_32x32x2_f32 (an
-// exact fp32 fma chain at 64 FLOP/clk/SIMD).  Operands are register-staged 16-B chunks into a
-// double-buffered [128 rows][16 k] image per operand whose 16-B chunks are XOR-swizzled by
-// (row >> 2) & 3, so the fragment reads (one ds_read_b128 per 4 MFMA k-steps: half-wave h takes
-// k = 8g + 4h + t at k-step 4g + t) are conflict-free.  The contraction order differs from the
-// 64x64 kernel's (fp32 rounding differences only).
+// fp32 kernel (parity mode: the forward, dX and dW products of the fp32 engine): 128x128x16 tile,
+// 4 waves of 64x64, v_mfma_f32_32x32x2_f32 (an exact fp32 fma chain at 64 FLOP/clk/SIMD).
+// Operands are register-staged 16-B chunks into double-buffered images, one per operand layout:
+//   K-contiguous (AK / BKC): [128 rows][16 k], 16-B chunks XOR-swizzled by (row >> 2) & 3, read as
+//     one ds_read_b128 per 4 MFMA k-steps (half-wave h takes k = 8g + 4h + t at k-step 4g + t);
+//   MN-contiguous: [16 k][128 rows] (the global rows as they are), read as one ds_read_b32 per
+//     k-step (32 consecutive rows per half-wave: conflict-free) in the same k order.
+// The contraction order differs from the 64x64 kernel's (fp32 rounding differences only).
 // ---------------------------------------------------------------------------
 namespace f32b {
 constexpr int BM = 128, BN = 128, BKT = 16;
 constexpr int IMG = BM * BKT * 4;  // 8 KiB per operand image
 __device__ __forceinline__ int off(int row, int ch) { return row * 64 + 16 * (ch ^ ((row >> 2) & 3)); }
+// stage one operand's 16 k x 128 rows: chunk c = tid + 256 i
+template <bool KC>
+__device__ __forceinline__ void load_op(float4 (&st)[2], const float* X, long long ld, int r0, int rlim, int k0,
+                                        int kend, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i;
+    if (KC) {
+      const int row = c >> 2, k = k0 + 4 * (c & 3), r = r0 + row;
+      st[i] = (r < rlim && k < kend) ? *(const float4*)(X + (long long)r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      const int kr = c >> 5, r = r0 + 4 * (c & 31), k = k0 + kr;  // rlim % 4 == 0 on this path
+      st[i] = (r < rlim && k < kend) ? *(const float4*)(X + (long long)k * ld + r) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+template <bool KC>
+__device__ __forceinline__ void store_op(const float4 (&st)[2], char* img, int tid) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int c = tid + 256 * i;
+    if (KC) *(float4*)(img + off(c >> 2, c & 3)) = st[i];
+    else *(float4*)(img + (c >> 5) * 512 + 16 * (c & 31)) = st[i];
+  }
+}
+// the 4 k-steps t = 0..3 of group g for the 32-row block at r0 (lane row r0 + (l & 31))
+template <bool KC>
+__device__ __forceinline__ float4 frag4(const char* img, int r0, int g, int lane) {
+  if (KC) return *(const float4*)(img + r0 * 64 + off(lane & 31, 2 * g + (lane >> 5)));  // r0 % 16 == 0
+  const float* col = (const float*)img + (8 * g + 4 * (lane >> 5)) * 128 + r0 + (lane & 31);
+  return make_float4(col[0], col[128], col[256], col[384]);
+}
 }  // namespace f32b
 
+template <bool AK, bool BKC>
 __global__ __launch_bounds__(256) void gemm_f32_big_kernel(GemmParams p) {
   using namespace f32b;
   __shared__ __attribute__((aligned(16))) char smem[4 * IMG];
@@ -193,24 +227,13 @@ __global__ __launch_bounds__(256) void gemm_f32_big_kernel(GemmParams p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   float4 sa[2], sb[2];
   auto load = [&](int k0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i, row = c >> 2, k = k0 + 4 * (c & 3);
-      const int m = m0 + row, n = n0 + row;
-      sa[i] = (m < p.M && k < kend) ? *(const float4*)(A + (long long)m * p.lda + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-      sb[i] = (n < p.N && k < kend) ? *(const float4*)(B + (long long)n * p.ldb + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    load_op<AK>(sa, A, p.lda, m0, p.M, k0, kend, tid);
+    load_op<BKC>(sb, B, p.ldb, n0, p.N, k0, kend, tid);
   };
   auto store = [&](char* img) __attribute__((always_inline)) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + 256 * i;
-      *(float4*)(img + off(c >> 2, c & 3)) = sa[i];
-      *(float4*)(img + IMG + off(c >> 2, c & 3)) = sb[i];
-    }
+    store_op<AK>(sa, img, tid);
+    store_op<BKC>(sb, img + IMG, tid);
   };
-  // per-lane fragment offsets: row (l & 31) of a 32-row block, chunk 2g + hl
-  const int ao[2] = {off(lane & 31, hl), off(lane & 31, 2 + hl)};
   load(kbeg);
   store(smem);
   __syncthreads();
@@ -224,8 +247,8 @@ __global__ __launch_bounds__(256) void gemm_f32_big_kernel(GemmParams p) {
       float4 a[2], b[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        a[i] = *(const float4*)(img + (wm + 32 * i) * 64 + ao[g]);
-        b[i] = *(const float4*)(img + IMG + (wn + 32 * i) * 64 + ao[g]);
+        a[i] = frag4<AK>(img, wm + 32 * i, g, lane);
+        b[i] = frag4<BKC>(img + IMG, wn + 32 * i, g, lane);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -627,10 +650,11 @@ struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC
 // 7.971 vs 8.034 and 8.05 vs 8.12 ms on two later boxes (3 x 2 and 2 x 3 interleaved runs, round 3):
 // mode 1 is the default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
 // products without an epilogue or with a bias only, 2 for every epilogue it implements.
-// CG_F32_BIG=0 routes K-contiguous fp32 products back to the 64x64 kernel (A/B switch)
+// fp32 products on the 128x128 f32-MFMA tile: 2 (default; env CG_F32_BIG) every operand layout,
+// 1 only K-contiguous x K-contiguous (the forward), 0 never (the 64x64 kernel: A/B switch)
 static int g_f32_big = [] {
   const char* e = getenv("CG_F32_BIG");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 2;
 }();
 static int g_pers_lw = [] {
   const char* e = getenv("CG_PERS_LW");
@@ -880,10 +904,16 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
 
   if (d->in_dtype == CG_F32) {
     p.epi &= ~CG_EPI_COLSUM;
-    if (d->a_kcontig && d->b_kcontig && !(d->lda & 3) && !(d->ldb & 3) && !(d->K & 3) &&
-        !((uintptr_t)d->A & 15) && !((uintptr_t)d->B & 15) && g_f32_big) {
-      hipLaunchKernelGGL(gemm_f32_big_kernel, dim3(cg_cdiv(p.N, f32b::BN), cg_cdiv(p.M, f32b::BM), split), dim3(256),
-                         0, s, p);
+    // the 128x128 f32-MFMA tile: 16-B operand chunks (leading dims and the contiguous extent of
+    // each operand -- K for a K-contiguous one, M / N for an MN-contiguous one -- multiples of 4)
+    const bool big = g_f32_big && !(d->lda & 3) && !(d->ldb & 3) && !((uintptr_t)d->A & 15) &&
+                     !((uintptr_t)d->B & 15) && ((d->a_kcontig || d->b_kcontig) ? !(d->K & 3) : true) &&
+                     (d->a_kcontig || !(d->M & 3)) && (d->b_kcontig || !(d->N & 3)) &&
+                     (g_f32_big > 1 || (d->a_kcontig && d->b_kcontig));
+    if (big) {
+      launch4(gemm_f32_big_kernel<false, false>, gemm_f32_big_kernel<false, true>, gemm_f32_big_kernel<true, false>,
+              gemm_f32_big_kernel<true, true>, d->a_kcontig, d->b_kcontig,
+              dim3(cg_cdiv(p.N, f32b::BN), cg_cdiv(p.M, f32b::BM), split), dim3(256), 0, s, p);
     } else {
       dim3 g(cg_cdiv(p.N, 64), cg_cdiv(p.M, 64), split);
       launch4(gemm_f32_kernel<false, false>, gemm_f32_kernel<false, true>, gemm_f32_kernel<true, false>,
