@@ -440,6 +440,13 @@ extern "C" int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, con
                                 dscale, scale, (const uint32_t*)drop_mask, bias_part, ld_part, s, rope_cos,
                                 rope_sin);
   }
+  // fp32: the f32-MFMA kernels (exact fp32 products; delta formed inside the dQ kernel) where the
+  // layout allows
+  if (dtype != CG_BF16 && attn_f32mfma_supported(hd, qkv, ldqkv, dy, lddy) && (lddqkv & 3) == 0 &&
+      ((uintptr_t)dqkv & 15) == 0 && (ldy & 3) == 0 && ((uintptr_t)y & 15) == 0)
+    return attn_bwd_f32mfma_launch((const float*)qkv, ldqkv, segstart, (const float*)dy, lddy, (const float*)y, ldy,
+                                   lse, delta, (float*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr, dscale,
+                                   scale, s);
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_delta_kernel<bf16_t>, dim3(cg_cdiv(nbt, 256)), dim3(256), 0, s, (const bf16_t*)y, ldy,
                        (const bf16_t*)dy, lddy, delta, B, T, H, hd);
@@ -448,11 +455,6 @@ extern "C" int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, con
                        (const float*)dy, lddy, delta, B, T, H, hd);
   }
   CG_LAUNCH_CHECK();
-  // fp32: the f32-MFMA kernels (exact fp32 products) where the layout allows
-  if (dtype != CG_BF16 && attn_f32mfma_supported(hd, qkv, ldqkv, dy, lddy) && (lddqkv & 3) == 0 &&
-      ((uintptr_t)dqkv & 15) == 0)
-    return attn_bwd_f32mfma_launch((const float*)qkv, ldqkv, segstart, (const float*)dy, lddy, lse, delta,
-                                   (float*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr, dscale, scale, s);
   dim3 gq(cg_cdiv(T, AV_TQ), B * H), gk(cg_cdiv(T, AV_TQ), B * KV);
   if (dtype == CG_BF16) {
     hipLaunchKernelGGL(attn_bwd_dq_vec<bf16_t>, gq, dim3(64), 0, s, (const bf16_t*)qkv, ldqkv, segstart,

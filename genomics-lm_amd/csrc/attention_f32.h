@@ -381,8 +381,9 @@ template <int DROP, int NG>
 __global__ __launch_bounds__(256, ATTN_F32B_WPS) void attn_bwd_dq_f32mfma(const float* __restrict__ qkv, long long ld,
                                                               const int32_t* __restrict__ seg,
                                                               const float* __restrict__ dy, long long lddy,
+                                                              const float* __restrict__ yo, long long ldy,
                                                               const float* __restrict__ lse,
-                                                              const float* __restrict__ delta, float* __restrict__ dqkv,
+                                                              float* __restrict__ delta, float* __restrict__ dqkv,
                                                               long long lddq, int T, int H, int KV, int hd, int window,
                                                               uint32_t seed, uint32_t thr, float dscale, float scale) {
   using namespace fa32;
@@ -401,7 +402,21 @@ __global__ __launch_bounds__(256, ATTN_F32B_WPS) void attn_bwd_dq_f32mfma(const 
   reg_rows(df, dy + (rowbase + (qok ? myq : 0)) * lddy + (long long)hh * hd, qok, NG, hl);
   const long long bhq = ((long long)b * H + hh) * T + (qok ? myq : 0);
   const float nl2 = qok ? -lse[bhq] * 1.4426950408889634f : 0.f;
-  const float dl = qok ? delta[bhq] : 0.f;
+  // delta = rowsum(dO o O) of the lane's query (the two half-waves hold complementary d), written
+  // for the dK / dV kernel
+  float dl;
+  {
+    float yv[8][4];
+    reg_rows(yv, yo + (rowbase + (qok ? myq : 0)) * ldy + (long long)hh * hd, qok, NG, hl);
+    float part = 0.f;
+#pragma unroll
+    for (int g = 0; g < 8; ++g)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) part = fmaf(df[g][t], yv[g][t], part);
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(part), __float_as_uint(part), false, false);
+    dl = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+    if (qok && hl == 0) delta[bhq] = dl;
+  }
   const int lo = qok ? fa::lo_of(seg, rowbase, myq, T, window) : 0x7fffffff;
   const int kmin = fa::lo_of(seg, rowbase, q0, T, window);
   const int kmax = min(T - 1, q0 + 127);
@@ -595,14 +610,15 @@ __global__ __launch_bounds__(256, ATTN_F32B_WPS) void attn_bwd_dkdv_f32mfma(cons
 }
 
 static inline int attn_bwd_f32mfma_launch(const float* qkv, long long ld, const int32_t* seg, const float* dy,
-                                          long long lddy, const float* lse, const float* delta, float* dqkv,
+                                          long long lddy, const float* y, long long ldy, const float* lse,
+                                          float* delta, float* dqkv,
                                           long long lddq, int B, int T, int H, int KV, int hd, int window,
                                           uint32_t seed, uint32_t thr, float dscale, float scale, hipStream_t s) {
   const dim3 gq(B * H, cg_cdiv(T, 128)), gk(B * KV, cg_cdiv(T, 128));
 #define CG_F32B(D, NG)                                                                                               \
   do {                                                                                                               \
-    hipLaunchKernelGGL((attn_bwd_dq_f32mfma<D, NG>), gq, dim3(256), 0, s, qkv, ld, seg, dy, lddy, lse, delta, dqkv, \
-                       lddq, T, H, KV, hd, window, seed, thr, dscale, scale);                                        \
+    hipLaunchKernelGGL((attn_bwd_dq_f32mfma<D, NG>), gq, dim3(256), 0, s, qkv, ld, seg, dy, lddy, y, ldy, lse,    \
+                       delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);                           \
     (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_f32mfma<D, NG>,                                         \
                               hipFuncAttributeMaxDynamicSharedMemorySize, fa32::LDS + fa32::QC_BYTES);               \
     hipLaunchKernelGGL((attn_bwd_dkdv_f32mfma<D, NG>), gk, dim3(256), fa32::LDS + fa32::QC_BYTES, s, qkv, ld, seg, \
