@@ -1,10 +1,10 @@
-# Round-3 evidence for one config: a bench line (with the live roofline probe), the rocprofv3
+# Round evidence (rounds 3, 4) for one config: a bench line (with the live roofline probe), the rocprofv3
 # kernel-trace stats of the bench command, the HBM PMC passes (FETCH_SIZE / WRITE_SIZE in separate
 # runs) and the kernel summary per step.
-#   bash tools/prof_round3.sh c4 [extra bench args]
+#   [ROUND=r4] bash tools/prof_round3.sh c4 [extra bench args]    -> gpurun_out/${ROUND:-r3}_<cfg>/
 set -u
 cfg=${1:-c4}; shift || true
-O=gpurun_out/r3_$cfg
+O=gpurun_out/${ROUND:-r3}_$cfg
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python bench.py --config $cfg "$@" > $O/bench.json 2> $O/bench.err &&
