@@ -649,7 +649,8 @@ struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC
 // whole C4 step measured 8.45 vs 8.41 ms on one box (bench.py, 2 x 2 interleaved runs) but
 // 7.971 vs 8.034 and 8.05 vs 8.12 ms on two later boxes (3 x 2 and 2 x 3 interleaved runs, round 3):
 // mode 1 is the default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
-// products without an epilogue or with a bias only, 2 for every epilogue it implements.
+// epilogues listed in pers_lw_for (round 4: widened from plain / bias-only), 2 for every epilogue it
+// implements.
 // fp32 products on the 128x128 f32-MFMA tile: 2 (default; env CG_F32_BIG) every operand layout,
 // 1 only K-contiguous x K-contiguous (the forward), 0 never (the 64x64 kernel: A/B switch)
 static int g_f32_big = [] {
@@ -686,7 +687,13 @@ static bool pers_lw_for(int e) {
   if (pers_pp_for(e)) return false;
   if (e & CG_EPI_ROPE) return g_pers_lw != 0;  // the RoPE epilogue is the loader-wave kernel's only
   if (g_pers_lw == 2) return e != CG_EPI_DSWIGLU;
-  return g_pers_lw == 1 && (e == 0 || e == CG_EPI_BIAS);
+  // mode 1: the epilogues measured faster on it (round 4, rocprofv3 per kernel, same box: C4 fc1
+  // forward GELU' 54.7 -> 52.0 us, proj forward bias + fp32 residual 23.5 -> 22.0, C3 SwiGLU forward
+  // 90.2 -> 87.4); the dGELU / dropout-residual / column-sum ones stay on the 8-wave kernel
+  // (C4 fc2 dX 52.1 -> 53.5, fc2 forward 49.8 -> 51.5 on it)
+  return g_pers_lw == 1 && (e == 0 || e == CG_EPI_BIAS || e == (CG_EPI_BIAS | CG_EPI_GELU) ||
+                            e == (CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV) ||
+                            e == (CG_EPI_BIAS | CG_EPI_RESID) || e == CG_EPI_RESID || e == CG_EPI_SWIGLU);
 }
 // the 256x256 ping-pong kernel (gemm_pp2.h) for bf16-output products with at least one 256-wide
 // column tile per CU-round: 0 off, 1 (env CG_PERS_PP2 at load)

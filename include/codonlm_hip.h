@@ -95,8 +95,9 @@ int cg_gemm_set_pers(int mode);
  * reserve.  cg_pers_cus: the CU count those launches (and the dW planner) use now. */
 int cg_set_cu_reserve(int n);
 /* persistent-tile variant with dedicated LDS-DMA loader waves (gemm_lw.h): 0 off, 1 (default; env
- * CG_PERS_LW at load) for products without an epilogue or with a bias only, 2 wherever it
- * implements the epilogue.  Returns the previous mode. */
+ * CG_PERS_LW at load) for the plain, bias, bias + GELU(') forward, fp32-residual and SwiGLU-forward
+ * products (the RoPE epilogue always), 2 wherever it implements the epilogue.  Returns the previous
+ * mode. */
 int cg_gemm_set_pers_lw(int mode);
 /* persistent-tile variant in which the two waves of each SIMD alternate MFMA and load segments
  * (gemm_pp.h): 0 off (default; env CG_PERS_PP at load), 1 for products without an epilogue or
