@@ -493,7 +493,7 @@ int transpose_weights(const Ctx& C) {
   return cg_transpose16_batch(&tb, C.s);
 }
 int pick_split(const Ctx& C, int Mo, int N, long long K) {
-  const int bm = C.dt == CG_BF16 ? 128 : 64;
+  const int bm = 128;  // the 128x128 tiles of the bf16 and (round 4: every layout) fp32 dW products
   const long long tiles = (long long)((Mo + bm - 1) / bm) * ((N + bm - 1) / bm);
   long long s = (512 + tiles - 1) / tiles;
   long long smax = K / 512;
