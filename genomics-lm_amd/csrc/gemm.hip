@@ -957,7 +957,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
       const int tiles = cg_cdiv(p.N, (p.epi & CG_EPI_SWIGLU) ? bfp::BN / 2 : bfp::BN) * cg_cdiv(p.M, bfp::BM);
       g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cg_pers_cus()));
       blk = dim3(pers_pp_for(p.epi) ? bpp::THREADS : pers_lw_for(p.epi) ? bfl::THREADS : bfp::THREADS);
-      sh = pers_pp_for(p.epi) ? bpp::SMEM : bfp::SMEM;
+      sh = pers_pp_for(p.epi) ? bpp::SMEM : pers_lw_for(p.epi) ? bfl::SMEM : bfp::SMEM;
     } else if (vec && use_wide(d, kchunk, split)) {
       k = pick_spec<WideK>(d->a_kcontig, d->b_kcontig, ke, kt);
       g = dim3(cg_cdiv(p.N, bfw::BN) * cg_cdiv(p.M, bfw::BM) * split);

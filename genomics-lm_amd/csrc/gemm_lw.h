@@ -26,11 +26,19 @@
 #ifndef CG_ROPE_DIAG
 #define CG_ROPE_DIAG 0
 #endif
+// A-operand L2 prefetch (experiment): the loaders also issue, per stage, 4-byte LDS-DMA reads of the
+// A rows CG_LW_PF stages ahead of the stage they stream (into a scratch slot nobody reads), so the
+// HBM misses of a tile's A rows are taken that far ahead; 0 = off
+#ifndef CG_LW_PF
+#define CG_LW_PF 0
+#endif
 namespace bfl {
 constexpr int CWAVES = 8, LWAVES = 4, THREADS = 64 * (CWAVES + LWAVES);
 constexpr int A_PIECES = bfw::A_BYTES / 1024, B_PIECES = bfw::B_BYTES / 1024;  // 32, 16 per stage
 constexpr int LA = A_PIECES / LWAVES, LB = B_PIECES / LWAVES;                  // 8, 4 per loader
 constexpr int PER_STAGE = LA + LB;                                             // DMAs per loader per stage
+constexpr int PF_OPS = CG_LW_PF ? LA : 0;                                      // prefetch reads per stage
+constexpr int SMEM = bfp::SMEM + (CG_LW_PF ? LWAVES * 256 : 0);
 }  // namespace bfl
 
 template <int EPI, int CT>
@@ -124,12 +132,26 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
       if constexpr (RP) {
         if ((g + 1) % nt == 0) rope_offsets((g + 1) / nt);
       }
+      if constexpr (CG_LW_PF > 0) {
+        const int gp = g + CG_LW_PF;
+        uint32_t po = OOR;
+        if (gp < S) {
+          const int k = gp / nt, t = gp - k * nt;
+          int m0, n0;
+          tile_org(k, m0, n0);
+          po = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
+        }
+        char* scr = smem + bfp::SMEM + L * 256;
+#pragma unroll
+        for (int j = 0; j < bfl::LA; ++j)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (bfw::lds_ptr_t)scr, 4, po == OOR ? OOR : po + va[j], 0, 0, 0);
+      }
     };
     if constexpr (RP) rope_offsets(0);
     issue(0);
     issue(1);
     for (int g = 0; g < S; ++g) {
-      wait_vm<bfl::PER_STAGE>();  // stage g landed; stage g+1 may still be in flight
+      wait_vm<bfl::PER_STAGE + 2 * bfl::PF_OPS>();  // stage g landed; stage g+1 may still be in flight
       __builtin_amdgcn_s_barrier();
       issue(g + 2);  // into the slot of stage g-1, whose reads retired before this barrier
     }
