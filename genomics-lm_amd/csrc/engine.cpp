@@ -243,6 +243,8 @@ struct Acts {
   std::vector<void*> oa, og, opj;
   // their backward dY operands, kept per head until one grouped dW launch takes all of them
   std::vector<void*> odpj, oda;
+  // their two d x d weights transposed (wT mode): K-contiguous dX operands, as the blocks'
+  std::vector<void*> o1T, o2T;
   // per offset head: its logits gradient (the layout of dlogits), stacked [head][M] like opj, so
   // the tied head's weight gradient over all heads is ONE product reduced over heads x tokens
   std::vector<void*> odl;
@@ -356,6 +358,13 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
       a.wguT = w.take<char>((size_t)d * 2 * D.Hp * 2);
       a.wdT = w.take<char>((size_t)D.Hp * d * 2);
     }
+  }
+  const int noffT = A.wT ? std::min(c->n_offsets, 8) : 0;
+  A.o1T.assign(noffT, nullptr);
+  A.o2T.assign(noffT, nullptr);
+  for (int i = 0; i < noffT; ++i) {
+    A.o1T[i] = w.take<char>((size_t)d * d * 2);
+    A.o2T[i] = w.take<char>((size_t)d * d * 2);
   }
   static const bool mask_env = [] { const char* e = getenv("CG_ATTN_DROP_MASK"); return !e || atoi(e) != 0; }();
   const bool dmask = mask_env && c->dtype == CG_BF16 && c->dropout > 0.f;
@@ -489,6 +498,10 @@ int transpose_weights(const Ctx& C) {
       CK(add(o.wgu, d, 2 * D.Hp, d, a.wguT));
       CK(add(o.wd, D.Hp, d, D.Hp, a.wdT));
     }
+  }
+  for (size_t i = 0; i < C.A.o1T.size(); ++i) {
+    CK(add(C.Lo.off1w[i], d, d, d, C.A.o1T[i]));
+    CK(add(C.Lo.off2w[i], d, d, d, C.A.o2T[i]));
   }
   return cg_transpose16_batch(&tb, C.s);
 }
@@ -784,13 +797,14 @@ int aux_backward(const Ctx& C, int accumulate) {
     CK(add_dw(dpj, A.og[i], C.Lo.off2w[i]));
     CK(defer_colsum(C, dpj, A.ocp[i], C.Lo.off2b[i], accumulate));
     // da = (dpj . W2) * gelu'(a) ; the first Linear's grads
-    g = lin_dx(C, dpj, d, C.Lo.off2w[i], d, d, d, da, d);
+    const bool hasT = i < (int)A.o2T.size();
+    g = lin_dx(C, dpj, d, C.Lo.off2w[i], d, d, d, da, d, hasT ? A.o2T[i] : nullptr);
     g.epilogue = CG_EPI_DGELU | CG_EPI_GELU_DERIV; g.aux = A.oa[i]; g.ld_aux = d;
     CK(cg_gemm(&g, C.s));
     CK(add_dw(da, A.xf, C.Lo.off1w[i]));
     CK(defer_colsum(C, da, A.ocp[i] + cg_colsum_workspace((int)M, d) / 4, C.Lo.off1b[i], accumulate));
     // dxf += da . W1
-    g = lin_dx(C, da, d, C.Lo.off1w[i], d, d, d, A.dtmp, d);
+    g = lin_dx(C, da, d, C.Lo.off1w[i], d, d, d, A.dtmp, d, hasT ? A.o1T[i] : nullptr);
     g.c_dtype = CG_F32;
     g.epilogue = CG_EPI_RESID; g.resid = A.dtmp; g.ldr = d;
     CK(cg_gemm(&g, C.s));
