@@ -72,7 +72,10 @@ static int dw_tile_for(const Dims& D, int n, double* cost_out) {
   double best_cost = 1e30;
   for (int bm : {128, 256, 512}) {
     if (dw_forced_bm() && bm != dw_forced_bm()) continue;
-    const double tile_cost = bm == 128 ? 1.0 : bm == 256 ? 1.38 : 2.35;
+    // (256 x 256: 2.35 at K = 16384 on C4/C5; 2.49 at C3, K = 32768: 951 vs 526 us per round of
+    // the 256 x 128 tile, rocprofv3 -- 2.5 keeps C4 on its 5/5/2 plan and moves C3 from 6/4 to
+    // 4/4/2, 9.08 -> 8.99 ms/step, profiles/round4/dw_sweep)
+    const double tile_cost = bm == 128 ? 1.0 : bm == 256 ? 1.38 : 2.5;
     const int per_layer = cg_gemm_dw_tiles(bm, D.Nqkv, d) + cg_gemm_dw_tiles(bm, d, d) +
                           (D.swiglu ? cg_gemm_dw_tiles(bm, 2 * D.Hp, d) + cg_gemm_dw_tiles(bm, d, D.Hp)
                                     : cg_gemm_dw_tiles(bm, D.hid, d) + cg_gemm_dw_tiles(bm, d, D.hid));
