@@ -28,6 +28,11 @@
 
 // ATTN_PRIO: raise a wave's issue priority while it issues its MFMA chains (s_setprio), so the
 // SIMD's other wave fills the gaps with VALU work instead of delaying them (A/B variant)
+// dK/dV body order (experiment): 0 = per 32-query half S, dP -> softmax / dS -> dV, dK; 1 = both
+// halves' S and dP first, so one half's VALU runs under the other half's MFMAs in the same wave
+#ifndef ATTN_DKDV_PIPE
+#define ATTN_DKDV_PIPE 0
+#endif
 #ifndef ATTN_PRIO
 #define ATTN_PRIO 0
 #endif
@@ -1001,90 +1006,115 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     // full: every (query, key) of the wave's tile visible.  Otherwise the invisible scores are
     // set to -inf before the exponent (the branch touches only s: the dK/dV accumulators keep
     // their registers across it)
-    auto body = [&](bool full) __attribute__((always_inline)) {
+    // phases of one 32-query half: S and dP (accumulators seeded with -lse2 / nd), the softmax,
+    // keep and dS in registers, then dV and dK
+    auto phase_sdp = [&](int qb, v16f& s, v16f& dp, v16f& nd) __attribute__((always_inline)) {
+      // dP starts from -delta/dscale (the rows' nd values): the accumulator then holds
+      // dP - delta/dscale, and dS/dscale = p * (keep ? acc : nd) is one bit-select and a multiply
+      // S starts from -lse2 (K is pre-multiplied by c = scale*log2(e)): the accumulator is the
+      // exp2 argument itself
 #pragma unroll
-      for (int qb = 0; qb < 2; ++qb) {
-        // dP starts from -delta/dscale (the rows' nd values): the accumulator then holds
-        // dP - delta/dscale, and dS/dscale = p * (keep ? acc : nd) is one bit-select and a multiply
-        // S starts from -lse2 (K is pre-multiplied by c = scale*log2(e)): the accumulator is the
-        // exp2 argument itself
-        v16f nd, s;
+      for (int rg = 0; rg < 16; rg += 4) {
+        const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
+        nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
+        const float4 l4 = *(const float4*)(lse2s + qb * 32 + acc_row(rg, lane));
+        s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
+      }
+      dp = nd;
+      ATTN_SETPRIO(1);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks < nks) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Qi, ro, qb * 32, ks), kf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
+        }
+      }
+      ATTN_SETPRIO(0);
+    };
+    auto phase_ds = [&](int qb, bool full, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1, v8bf& sb0,
+                        v8bf& sb1) __attribute__((always_inline)) {
+      if (!full) {
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 4) {
-          const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
-          nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
-          const float4 l4 = *(const float4*)(lse2s + qb * 32 + acc_row(rg, lane));
-          s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
-        }
-        v16f dp = nd;
-        ATTN_SETPRIO(1);
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          if (ks < nks) {
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Qi, ro, qb * 32, ks), kf[ks], s, 0, 0, 0);
-            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
-          }
-        }
-        ATTN_SETPRIO(0);
-        if (!full) {
-#pragma unroll
-          for (int rg = 0; rg < 16; rg += 4) {
-            const int qi = qb * 32 + acc_row(rg, lane);
-            const int4 lo4 = *(const int4*)(los + qi);
-            const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int q = q0 + qi + u;
-              const int lq = window > 0 ? max(lov[u], q - window + 1) : lov[u];
-              s[rg + u] = ((mykey > q) | (mykey < lq) | (q >= T)) ? -INFINITY : s[rg + u];
-            }
-          }
-        }
-        v16f pd;
-#pragma unroll
-        for (int rg = 0; rg < 16; rg += 4) {
-          const int qi = qb * 32 + acc_row(rg, lane);  // 4 consecutive queries qi..qi+3
-          uint4 hr4 = make_uint4(0, 0, 0, 0);
-          if constexpr (DROP == 1) hr4 = *(const uint4*)(hrs + qi);
-          uint4 mw4 = make_uint4(0, 0, 0, 0);
-          if constexpr (DROP == 2) mw4 = *(const uint4*)(mws + qi);
-          const uint32_t mwv[4] = {mw4.x, mw4.y, mw4.z, mw4.w};
-          const uint32_t hrv[4] = {hr4.x, hr4.y, hr4.z, hr4.w};
+          const int qi = qb * 32 + acc_row(rg, lane);
+          const int4 lo4 = *(const int4*)(los + qi);
+          const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const int r = rg + u;
-            const float p = __builtin_amdgcn_exp2f(s[r]);
-            float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
-            if constexpr (DROP == 1) {
-              const uint32_t hsh = cg_pair_mix(hrv[u] + kcol);
-              const uint32_t bits = (mykey & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
-              const bool keep = bits >= thr;
-              pdr = keep ? p : 0.f;
-              s[r] = p * (keep ? dp[r] : nd[r]);
-            } else if constexpr (DROP == 2) {
-              const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
-              pdr = __uint_as_float(__float_as_uint(p) & m);
-              s[r] = p * __uint_as_float((__float_as_uint(dp[r]) & m) | (__float_as_uint(nd[r]) & ~m));
-            } else {
-              s[r] = p * dp[r];
-            }
-            pd[r] = pdr;
+            const int q = q0 + qi + u;
+            const int lq = window > 0 ? max(lov[u], q - window + 1) : lov[u];
+            s[rg + u] = ((mykey > q) | (mykey < lq) | (q >= T)) ? -INFINITY : s[rg + u];
           }
         }
-        const v8bf pb0 = pack_b(pd, 0), pb1 = pack_b(pd, 1);
-        const v8bf sb0 = pack_b(s, 0), sb1 = pack_b(s, 1);
-        ATTN_SETPRIO(1);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 0), pb0, dv0, 0, 0, 0);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 0), pb1, dv0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 0), sb0, dk0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 0), sb1, dk0, 0, 0, 0);
-        if constexpr (hd > 32) {
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 1), pb0, dv1, 0, 0, 0);
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 1), pb1, dv1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 1), sb0, dk1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 1), sb1, dk1, 0, 0, 0);
+      }
+      v16f pd;
+#pragma unroll
+      for (int rg = 0; rg < 16; rg += 4) {
+        const int qi = qb * 32 + acc_row(rg, lane);  // 4 consecutive queries qi..qi+3
+        uint4 hr4 = make_uint4(0, 0, 0, 0);
+        if constexpr (DROP == 1) hr4 = *(const uint4*)(hrs + qi);
+        uint4 mw4 = make_uint4(0, 0, 0, 0);
+        if constexpr (DROP == 2) mw4 = *(const uint4*)(mws + qi);
+        const uint32_t mwv[4] = {mw4.x, mw4.y, mw4.z, mw4.w};
+        const uint32_t hrv[4] = {hr4.x, hr4.y, hr4.z, hr4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rg + u;
+          const float p = __builtin_amdgcn_exp2f(s[r]);
+          float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
+          if constexpr (DROP == 1) {
+            const uint32_t hsh = cg_pair_mix(hrv[u] + kcol);
+            const uint32_t bits = (mykey & 1) ? (hsh >> 16) : (hsh & 0xFFFFu);
+            const bool keep = bits >= thr;
+            pdr = keep ? p : 0.f;
+            s[r] = p * (keep ? dp[r] : nd[r]);
+          } else if constexpr (DROP == 2) {
+            const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
+            pdr = __uint_as_float(__float_as_uint(p) & m);
+            s[r] = p * __uint_as_float((__float_as_uint(dp[r]) & m) | (__float_as_uint(nd[r]) & ~m));
+          } else {
+            s[r] = p * dp[r];
+          }
+          pd[r] = pdr;
         }
-        ATTN_SETPRIO(0);
+      }
+      pb0 = pack_b(pd, 0); pb1 = pack_b(pd, 1);
+      sb0 = pack_b(s, 0); sb1 = pack_b(s, 1);
+    };
+    auto phase_dkdv = [&](int qb, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
+                          __attribute__((always_inline)) {
+      ATTN_SETPRIO(1);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 0), pb0, dv0, 0, 0, 0);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 0), pb1, dv0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 0), sb0, dk0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 0), sb1, dk0, 0, 0, 0);
+      if constexpr (hd > 32) {
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 1), pb0, dv1, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 1), pb1, dv1, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 1), sb0, dk1, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 1), sb1, dk1, 0, 0, 0);
+      }
+      ATTN_SETPRIO(0);
+    };
+    auto body = [&](bool full) __attribute__((always_inline)) {
+      if constexpr (ATTN_DKDV_PIPE) {
+        v16f s0, dp0, nd0, s1, dp1, nd1;
+        v8bf a0, a1, a2, a3, b0, b1, b2, b3;
+        phase_sdp(0, s0, dp0, nd0);
+        phase_sdp(1, s1, dp1, nd1);
+        phase_ds(0, full, s0, dp0, nd0, a0, a1, a2, a3);
+        phase_dkdv(0, a0, a1, a2, a3);
+        phase_ds(1, full, s1, dp1, nd1, b0, b1, b2, b3);
+        phase_dkdv(1, b0, b1, b2, b3);
+      } else {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          v16f s, dp, nd;
+          v8bf x0, x1, x2, x3;
+          phase_sdp(qb, s, dp, nd);
+          phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
+          phase_dkdv(qb, x0, x1, x2, x3);
+        }
       }
     };
     if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0));
