@@ -169,19 +169,27 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmParams p) {
 //     k-step (32 consecutive rows per half-wave: conflict-free) in the same k order.
 // The contraction order differs from the 64x64 kernel's (fp32 rounding differences only).
 // ---------------------------------------------------------------------------
+#ifndef CG_F32_BK
+#define CG_F32_BK 16
+#endif
 namespace f32b {
-constexpr int BM = 128, BN = 128, BKT = 16;
-constexpr int IMG = BM * BKT * 4;  // 8 KiB per operand image
-__device__ __forceinline__ int off(int row, int ch) { return row * 64 + 16 * (ch ^ ((row >> 2) & 3)); }
-// stage one operand's 16 k x 128 rows: chunk c = tid + 256 i
+constexpr int BM = 128, BN = 128, BKT = CG_F32_BK;  // k per stage: 16 or 32
+constexpr int RB = BKT * 4;                        // bytes per K-contiguous image row
+constexpr int CPR = BKT / 4;                       // 16-B chunks per such row
+constexpr int NCH = BM * BKT / 4 / 256;            // chunks per thread per operand
+constexpr int IMG = BM * BKT * 4;                  // bytes per operand image
+// chunk swizzle: conflict-free ds_read_b128 of 32 consecutive rows (16-lane groups hit 64 banks)
+__device__ __forceinline__ int swz(int row) { return CPR == 4 ? ((row >> 2) & 3) : ((row >> 1) & 7); }
+__device__ __forceinline__ int off(int row, int ch) { return row * RB + 16 * (ch ^ swz(row)); }
+// stage one operand's BKT k x 128 rows: chunk c = tid + 256 i
 template <bool KC>
-__device__ __forceinline__ void load_op(float4 (&st)[2], const float* X, long long ld, int r0, int rlim, int k0,
+__device__ __forceinline__ void load_op(float4 (&st)[NCH], const float* X, long long ld, int r0, int rlim, int k0,
                                         int kend, int tid) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NCH; ++i) {
     const int c = tid + 256 * i;
     if (KC) {
-      const int row = c >> 2, k = k0 + 4 * (c & 3), r = r0 + row;
+      const int row = c / CPR, k = k0 + 4 * (c % CPR), r = r0 + row;
       st[i] = (r < rlim && k < kend) ? *(const float4*)(X + (long long)r * ld + k) : make_float4(0.f, 0.f, 0.f, 0.f);
     } else {
       const int kr = c >> 5, r = r0 + 4 * (c & 31), k = k0 + kr;  // rlim % 4 == 0 on this path
@@ -190,18 +198,18 @@ __device__ __forceinline__ void load_op(float4 (&st)[2], const float* X, long lo
   }
 }
 template <bool KC>
-__device__ __forceinline__ void store_op(const float4 (&st)[2], char* img, int tid) {
+__device__ __forceinline__ void store_op(const float4 (&st)[NCH], char* img, int tid) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < NCH; ++i) {
     const int c = tid + 256 * i;
-    if (KC) *(float4*)(img + off(c >> 2, c & 3)) = st[i];
+    if (KC) *(float4*)(img + off(c / CPR, c % CPR)) = st[i];
     else *(float4*)(img + (c >> 5) * 512 + 16 * (c & 31)) = st[i];
   }
 }
 // the 4 k-steps t = 0..3 of group g for the 32-row block at r0 (lane row r0 + (l & 31))
 template <bool KC>
 __device__ __forceinline__ float4 frag4(const char* img, int r0, int g, int lane) {
-  if (KC) return *(const float4*)(img + r0 * 64 + off(lane & 31, 2 * g + (lane >> 5)));  // r0 % 16 == 0
+  if (KC) return *(const float4*)(img + r0 * RB + off(lane & 31, 2 * g + (lane >> 5)));  // r0 % 16 == 0
   const float* col = (const float*)img + (8 * g + 4 * (lane >> 5)) * 128 + r0 + (lane & 31);
   return make_float4(col[0], col[128], col[256], col[384]);
 }
@@ -225,7 +233,7 @@ __global__ __launch_bounds__(256) void gemm_f32_big_kernel(GemmParams p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  float4 sa[2], sb[2];
+  float4 sa[NCH], sb[NCH];
   auto load = [&](int k0) __attribute__((always_inline)) {
     load_op<AK>(sa, A, p.lda, m0, p.M, k0, kend, tid);
     load_op<BKC>(sb, B, p.ldb, n0, p.N, k0, kend, tid);
@@ -243,7 +251,7 @@ __global__ __launch_bounds__(256) void gemm_f32_big_kernel(GemmParams p) {
     if (more) load(k0 + BKT);
     const char* img = smem + cur * 2 * IMG;
 #pragma unroll
-    for (int g = 0; g < 2; ++g) {
+    for (int g = 0; g < BKT / 8; ++g) {
       float4 a[2], b[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
