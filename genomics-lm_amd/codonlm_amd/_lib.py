@@ -68,7 +68,8 @@ class DwProduct(C.Structure):
 
 
 class DwGroup(C.Structure):
-    _fields_ = [("n", i32), ("K", i32), ("tile_m", i32), ("p", DwProduct * DW_MAX)]
+    _fields_ = [("n", i32), ("K", i32), ("tile_m", i32), ("p", DwProduct * DW_MAX),
+                ("ksplit", i32), ("workspace", vp), ("ws_bytes", sz)]
 
 
 REDUCE_MAX = 48
@@ -137,6 +138,7 @@ SIGNATURES = {
     "cg_set_dw_group": (i32, [i32]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),
+    "cg_gemm_dw_grouped_workspace": (sz, [C.POINTER(DwGroup)]),
     "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),
     "cg_gemm_dw_tiles": (i32, [i32, i32, i32]),
     "cg_gemm_dw_set_tile": (i32, [i32]),

@@ -368,10 +368,11 @@ def transpose16(mats):
     return outs
 
 
-def gemm_dw_grouped(products, *, tile_m=0):
+def gemm_dw_grouped(products, *, tile_m=0, ksplit=1):
     """Grouped weight gradients: for each (dy [K, N_out] bf16, x [K, K_out] bf16, out fp32
     [N_out, K_out], alpha, accumulate) -> out (+)= alpha * dy^T x, one persistent launch
-    (cg_gemm_dw_grouped).  Row strides are taken from the tensors."""
+    (cg_gemm_dw_grouped).  Row strides are taken from the tensors.  ksplit > 1: each tile's K rows
+    split over that many workgroups (fp32 slabs + one in-order reduction)."""
     if not products:
         return
     if len(products) > L.DW_MAX:
@@ -396,4 +397,11 @@ def gemm_dw_grouped(products, *, tile_m=0):
             raise ValueError("gemm_dw_grouped: out must be [N_out, K_out]")
         p.alpha, p.accumulate = float(alpha), int(bool(acc))
     g.K = int(K)
+    ws = None
+    if ksplit > 1:
+        g.ksplit = int(ksplit)
+        nbytes = int(L.lib.cg_gemm_dw_grouped_workspace(C.byref(g)))
+        ws = torch.empty(max(nbytes, 16) // 4, dtype=torch.float32, device=products[0][0].device)
+        g.workspace, g.ws_bytes = ws.data_ptr(), ws.numel() * 4
     L.check(L.lib.cg_gemm_dw_grouped(C.byref(g), L.stream_ptr(products[0][0].device)), "cg_gemm_dw_grouped")
+    return ws

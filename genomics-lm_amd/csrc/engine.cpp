@@ -25,7 +25,7 @@ enum { SITE_EMB = 0, SITE_ATTN = 1, SITE_MLP = 2 };
 
 struct Dims {
   int V, Vp, Tmax, L, H, KV, d, hd, kvd, Nqkv, hid, Hp, swiglu, rope;
-  int G, dw_bm;  // blocks per grouped weight-gradient launch and its tile rows (dw_plan)
+  int G, dw_bm, dw_ks;  // blocks per grouped weight-gradient launch, its tile rows, token split
 };
 
 bool dims_of(const cg_model_cfg* c, Dims& D) {
@@ -46,6 +46,7 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   D.Hp = D.swiglu ? (int)rup(D.hid, 64) : D.hid;
   D.G = 1;
   D.dw_bm = 128;
+  D.dw_ks = 1;
   return true;
 }
 
@@ -59,16 +60,29 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
 // summed cost of the groups (G, G, ..., remainder) and, on ties, prefers the smaller group (its
 // gradients are final -- and all-reduced -- earlier).  CG_DW_GROUP / CG_DW_BM force a choice.
 struct DwPlan {
-  int G, bm;  // group size, tile of a full group
+  int G, bm, ks;  // group size, tile of a full group, its token-range split
 };
 static int dw_forced_bm() {
   static const int forced = [] { const char* e = getenv("CG_DW_BM"); return e ? atoi(e) : 0; }();
   return forced;
 }
-// cheapest tile for a group of n blocks, and its cost
-static int dw_tile_for(const Dims& D, int n, double* cost_out) {
+static int dw_forced_ks() {
+  static const int forced = [] { const char* e = getenv("CG_DW_KSPLIT"); return e ? atoi(e) : 0; }();
+  return forced;
+}
+// weight elements of one block's dW products (the slab a token-range split writes per slice)
+static long long dw_block_elems(const Dims& D) {
+  const long long d = D.d;
+  return (long long)D.Nqkv * d + d * d + (D.swiglu ? 3LL * D.Hp * d : 2LL * D.hid * d);
+}
+// cheapest (tile, token-range split) for a group of n blocks over M tokens, and its cost.  A split
+// into ks slices makes ks x more work items of 1/ks the k-steps (more rounds filled where the
+// tiles alone leave CUs idle: C2's 144 tiles on 256 CUs) plus a slab pass of ~20 B per weight
+// element and extra slice at ~5 TB/s, priced against ~11 ns per token for 1.0 of tile cost
+// (C2 / C3 rocprofv3: 495 us for a round of 1.38 at M = 32768)
+static int dw_tile_for(const Dims& D, int n, double* cost_out, int* ks_out = nullptr, long long M = 16384) {
   const int d = D.d, cus = cg_pers_cus();
-  int best = 256;
+  int best = 256, best_ks = 1;
   double best_cost = 1e30;
   for (int bm : {128, 256, 512}) {
     if (dw_forced_bm() && bm != dw_forced_bm()) continue;
@@ -79,29 +93,39 @@ static int dw_tile_for(const Dims& D, int n, double* cost_out) {
     const int per_layer = cg_gemm_dw_tiles(bm, D.Nqkv, d) + cg_gemm_dw_tiles(bm, d, d) +
                           (D.swiglu ? cg_gemm_dw_tiles(bm, 2 * D.Hp, d) + cg_gemm_dw_tiles(bm, d, D.Hp)
                                     : cg_gemm_dw_tiles(bm, D.hid, d) + cg_gemm_dw_tiles(bm, d, D.hid));
-    const double cost = (double)((n * per_layer + cus - 1) / cus) * tile_cost;
-    if (cost < best_cost - 1e-9) best_cost = cost, best = bm;
+    for (int ks = 1; ks <= 3; ++ks) {
+      if (dw_forced_ks() && ks != dw_forced_ks()) continue;
+      const double slab = (double)(ks - 1) * n * dw_block_elems(D) * 20.0 / 5e12 / (11e-9 * (double)M);
+      const double cost = (double)((n * per_layer * ks + cus - 1) / cus) * tile_cost / ks + slab;
+      if (cost < best_cost - 1e-9) best_cost = cost, best = bm, best_ks = ks;
+    }
   }
   if (cost_out) *cost_out = best_cost;
+  if (ks_out) *ks_out = best_ks;
   return best;
 }
 static int g_dw_group = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
 static int g_dw_order = [] { const char* e = getenv("CG_DW_ORDER"); return e ? atoi(e) : 1; }();
-DwPlan dw_plan(const cg_model_cfg* c, const Dims& D) {
-  if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128};
+DwPlan dw_plan(const cg_model_cfg* c, const Dims& D, long long M = 16384) {
+  if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128, 1};
   const int forced_g = g_dw_group;
   const int gmax = std::min(D.L, CG_DW_MAX / 4);
-  DwPlan best{1, 128};
+  DwPlan best{1, 128, 1};
   double best_cost = 1e30;
   for (int g = 1; g <= gmax; ++g) {
     if (forced_g && g != std::min(forced_g, gmax)) continue;
     double cost = 0;
     for (int left = D.L; left > 0; left -= g) {
       double cg;
-      dw_tile_for(D, std::min(g, left), &cg);
+      dw_tile_for(D, std::min(g, left), &cg, nullptr, M);
       cost += cg;
     }
-    if (cost < best_cost - 1e-9) best_cost = cost, best = {g, dw_tile_for(D, g, nullptr)};
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      int ks = 1;
+      const int bm = dw_tile_for(D, g, nullptr, &ks, M);
+      best = {g, bm, ks};
+    }
   }
   return best;
 }
@@ -224,7 +248,7 @@ struct DwSlot {
 };
 // byte sizes of the carved scratch buffers handed to the op entry points (their ws_bytes)
 struct WsBytes {
-  size_t lnp, cpart, colws, splitws, embws, cews, delta, ocp_half;
+  size_t lnp, cpart, colws, splitws, embws, cews, delta, ocp_half, dwslab;
 };
 struct Acts {
   int32_t* seg;
@@ -239,6 +263,7 @@ struct Acts {
   long long ldl;  // dlogits row stride: Vp, or 2 Vp for split bf16 (hi | lo)
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
   float* bpart;  // qkv bias-gradient partials from the attention backward [B*ceil(T/128)][Nqkv]
+  float* dwslab;  // bf16: the grouped dW's token-split slabs (null when no group splits)
   size_t splitws_floats;
   WsBytes nb;
   bool wT;  // transposed weight copies present
@@ -342,6 +367,22 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.splitws_floats = std::max<size_t>(A.splitws_floats, (size_t)((M + 63) / 64) * (size_t)big);
   A.nb.splitws = A.splitws_floats * 4;
   A.splitws = w.take<float>(A.nb.splitws);
+  // grouped-dW token-split slabs: (ks - 1) slices of a group's weights (+ the tied head's, which
+  // can join the first group), for the larger of the full group's and the remainder's split
+  A.dwslab = nullptr;
+  A.nb.dwslab = 0;
+  if (c->dtype == CG_BF16 && D.L > 0) {
+    const int rem = D.L % D.G;
+    int ks_rem = 1;
+    if (rem) dw_tile_for(D, rem, nullptr, &ks_rem, M);
+    const long long head = (long long)D.Vp * d;
+    const long long need = std::max<long long>((long long)(D.dw_ks - 1) * (D.G * dw_block_elems(D) + head),
+                                               (long long)(ks_rem - 1) * (rem * dw_block_elems(D) + head));
+    if (need > 0) {
+      A.nb.dwslab = (size_t)need * 4;
+      A.dwslab = w.take<float>(A.nb.dwslab);
+    }
+  }
   A.nb.embws = cg_embed_bwd_workspace((int)B, (int)T, D.V, d);  // bytes, sized by the kernel's own chunking
   A.embws = w.take<float>(A.nb.embws);
   A.nb.cews = cg_ce_workspace((int)M);
@@ -389,9 +430,10 @@ struct Ctx {
 
 int make_ctx(const cg_model* m, int B, int T, void* stream, Ctx& C) {
   if (!dims_of(&m->cfg, C.D)) return CG_EINVAL;
-  const DwPlan pl = dw_plan(&m->cfg, C.D);
+  const DwPlan pl = dw_plan(&m->cfg, C.D, (long long)B * T);
   C.D.G = pl.G;
   C.D.dw_bm = pl.bm;
+  C.D.dw_ks = pl.ks;
   build_layout(&m->cfg, C.D, C.Lo);
   C.m = m;
   C.B = B; C.T = T; C.M = (long long)B * T;
@@ -679,7 +721,13 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
   cg_dw_group grp;
   memset(&grp, 0, sizeof(grp));
   grp.K = (int)C.M;
-  grp.tile_m = l_hi - l_lo + 1 == D.G ? D.dw_bm : dw_tile_for(D, l_hi - l_lo + 1, nullptr);
+  int ks = D.dw_ks;
+  grp.tile_m = l_hi - l_lo + 1 == D.G ? D.dw_bm : dw_tile_for(D, l_hi - l_lo + 1, nullptr, &ks, C.M);
+  if (ks > 1 && C.A.dwslab) {
+    grp.ksplit = ks;
+    grp.workspace = C.A.dwslab;
+    grp.ws_bytes = C.A.nb.dwslab;
+  }
   auto add = [&](const void* dy, int n_out, const void* x, int k_out, long long goff) -> int {
     if (C.dt != CG_BF16) return lin_dw(C, dy, n_out, x, k_out, n_out, k_out, goff, k_out, accumulate);
     cg_dw_product& q = grp.p[grp.n++];
@@ -879,9 +927,10 @@ extern "C" int cg_model_dw_plan(const cg_model_cfg* cfg, int* group_layers, int*
 extern "C" size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T) {
   Dims D;
   if (!dims_of(cfg, D)) return 0;
-  const DwPlan pl = dw_plan(cfg, D);
+  const DwPlan pl = dw_plan(cfg, D, (long long)B * T);
   D.G = pl.G;
   D.dw_bm = pl.bm;
+  D.dw_ks = pl.ks;
   Acts A;
   return carve(cfg, D, B, T, nullptr, A);
 }

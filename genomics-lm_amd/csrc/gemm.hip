@@ -1055,9 +1055,10 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
     pr.tile0 = ntiles;
     ntiles += cg_cdiv(pr.N_out, BM) * pr.tiles_n;
   }
-  P.ntiles = ntiles;
+  P.ntiles = ntiles * P.ksplit;
   if (!ntiles) return CG_OK;
-  const int grid = std::min(ntiles, cg_pers_cus());
+  if (P.ksplit > 1) P.kc_steps = cg_cdiv(cg_cdiv(P.K, P.ksplit), bfd::BKT);
+  const int grid = std::min(P.ntiles, cg_pers_cus());
   (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G::SMEM);
   double flops = 0, bytes = 0;
@@ -1068,10 +1069,25 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   }
   cg_probe_begin(CG_PROBE_GEMM_DW_GROUPED, s);
   hipLaunchKernelGGL((gemm_dw_kernel<BM, NS, BNT>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
+  if (P.ksplit > 1) {
+    long long most = 0;
+    for (int i = 0; i < P.nprod; ++i) most = std::max<long long>(most, (long long)P.p[i].N_out * P.p[i].K_out / 4);
+    hipLaunchKernelGGL(dw_slab_reduce_kernel, dim3((unsigned)std::min<long long>(cg_cdiv(most, 256), 512), P.nprod),
+                       dim3(256), 0, s, P);
+  }
   cg_probe_end(CG_PROBE_GEMM_DW_GROUPED, s, flops, bytes);
   CG_LAUNCH_CHECK();
   return CG_OK;
 }
+// slab bytes cg_gemm_dw_grouped needs for grp->ksplit > 1
+extern "C" size_t cg_gemm_dw_grouped_workspace(const cg_dw_group* grp) {
+  if (!grp || grp->ksplit <= 1) return 0;
+  size_t e = 0;
+  for (int i = 0; i < grp->n && i < CG_DW_MAX; ++i)
+    if (grp->p[i].N_out > 0 && grp->p[i].K_out > 0) e += (size_t)grp->p[i].N_out * (size_t)grp->p[i].K_out;
+  return (size_t)(grp->ksplit - 1) * e * sizeof(float);
+}
+extern "C" size_t cg_gemm_dw_grouped_workspace(const cg_dw_group* grp);
 extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
   if (!grp || grp->n < 0 || grp->n > CG_DW_MAX || grp->K <= 0) return CG_EINVAL;
   bfd::Params P{};
@@ -1096,6 +1112,19 @@ extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
     pr.alpha = q.alpha; pr.accum = q.accumulate;
   }
   if (!P.nprod) return CG_OK;
+  P.ksplit = grp->ksplit > 1 ? grp->ksplit : 1;
+  if (P.ksplit > 8) return CG_EUNSUPPORTED;
+  if (P.ksplit > 1) {
+    if (!grp->workspace || ((uintptr_t)grp->workspace & 15) || grp->ws_bytes < cg_gemm_dw_grouped_workspace(grp))
+      return CG_EINVAL;
+    P.slab = grp->workspace;
+    long long off = 0;
+    for (int i = 0; i < P.nprod; ++i) {
+      P.slab_off[i] = off;
+      off += (long long)P.p[i].N_out * P.p[i].K_out;
+    }
+    P.slab_stride = off;
+  }
   hipStream_t s = (hipStream_t)stream;
   const int bm = grp->tile_m > 0 ? grp->tile_m : g_dw_bm;
   // tile_m codes: 128 / 256 = rows of the C tile (ring of 4 / 3 stages); 129 / 257 = the same

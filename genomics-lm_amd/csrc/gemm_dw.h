@@ -69,7 +69,15 @@ struct Prod {
 };
 struct Params {
   Prod p[CG_DW_MAX];
-  int nprod, K, ntiles;
+  int nprod, K, ntiles;  // ntiles: work items = output tiles x ksplit
+  // split of the token range (round 4): item = tile * ksplit + s covers rows [s kc, (s+1) kc) of K
+  // (kc = kc_steps k-steps); slice 0 writes C as before, slices s >= 1 write fp32 slab s-1
+  // ([N_out][K_out] at slab + (s-1) slab_stride + the product's slab_off), added into C by
+  // dw_slab_reduce_kernel in slice order
+  int ksplit, kc_steps;
+  float* slab;
+  long long slab_stride;
+  long long slab_off[CG_DW_MAX];
 };
 }  // namespace bfd
 
@@ -86,7 +94,9 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
   const int nblk = gridDim.x;
   const int lb = cg_xcd_remap(blockIdx.x, nblk);  // an XCD's workgroups take consecutive tiles
   const int my_tiles = lb < P.ntiles ? (P.ntiles - 1 - lb) / nblk + 1 : 0;
-  const int nt = (P.K + BKT - 1) / BKT;  // a ragged last step reads rows >= K out of range: zero fill
+  // k-steps per work item (a ragged last step -- and a last slice past K -- reads rows >= K out of
+  // range: zero fill)
+  const int nt = P.ksplit > 1 ? P.kc_steps : (P.K + BKT - 1) / BKT;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * (BNT / 2);
   if (my_tiles == 0) return;
 
@@ -107,7 +117,8 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
       return;
     }
     int pi;
-    const int tile = lb + dk * nblk;
+    const int item = lb + dk * nblk;
+    const int tile = item / P.ksplit, sl = item - tile * P.ksplit;
     find(tile, pi);
     const Prod& pr = P.p[pi];
     const int lt = tile - pr.tile0;
@@ -116,8 +127,9 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
                                            (int)(((long long)(P.K - 1) * pr.lda + pr.N_out) * 2), 0x00020000);
     rb = __builtin_amdgcn_make_buffer_rsrc((void*)pr.B, (short)0,
                                            (int)(((long long)(P.K - 1) * pr.ldb + pr.K_out) * 2), 0x00020000);
-    a_org = (uint32_t)m0 * 2;
-    b_org = (uint32_t)n0 * 2;
+    const long long r0 = (long long)sl * nt * BKT;  // first token row of the slice
+    a_org = (uint32_t)((long long)m0 * 2 + r0 * pr.lda * 2);
+    b_org = (uint32_t)((long long)n0 * 2 + r0 * pr.ldb * 2);
     a_step = (uint32_t)(BKT * pr.lda * 2);
     b_step = (uint32_t)(BKT * pr.ldb * 2);
 #pragma unroll
@@ -213,13 +225,30 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
   };
 
   auto epilogue = [&](int k) {
-    const int tile = lb + k * nblk;
+    const int item = lb + k * nblk;
+    const int tile = item / P.ksplit, sl = item - tile * P.ksplit;
     int pi;
     find(tile, pi);
     const Prod& pr = P.p[pi];
     const int lt = tile - pr.tile0;
     const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BNT;
     const int g4 = lane >> 4, r16 = lane & 15;
+    if (sl > 0) {  // a later token slice: its partial to the slab (dense [N_out][K_out])
+      float* slab = P.slab + (long long)(sl - 1) * P.slab_stride + P.slab_off[pi];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm + 16 * i + r16;
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          const int n = n0 + wn + 16 * j + 4 * g4;
+          if (m < pr.N_out && n < pr.K_out)
+            *(float4*)(slab + (long long)m * pr.K_out + n) =
+                make_float4(acc[i][j][0] * pr.alpha, acc[i][j][1] * pr.alpha, acc[i][j][2] * pr.alpha,
+                            acc[i][j][3] * pr.alpha);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm + 16 * i + r16;
@@ -254,3 +283,23 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
 }
+
+// C_p += sum over slabs 1 .. ksplit-1 (slice order, after slice 0's C update): one workgroup row
+// per product (blockIdx.y), 4 consecutive columns per thread
+__global__ __launch_bounds__(256) void dw_slab_reduce_kernel(const bfd::Params P) {
+  const bfd::Prod& pr = P.p[blockIdx.y];
+  const float* slab = P.slab + P.slab_off[blockIdx.y];
+  const long long n4 = (long long)pr.N_out * pr.K_out / 4;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n4; e += (long long)gridDim.x * 256) {
+    const long long idx = 4 * e;
+    const int m = (int)(idx / pr.K_out), n = (int)(idx - (long long)m * pr.K_out);
+    float4* c = (float4*)(pr.C + (long long)m * pr.ldc + n);
+    float4 v = *c;
+    for (int s = 1; s < P.ksplit; ++s) {
+      const float4 w = *(const float4*)(slab + (long long)(s - 1) * P.slab_stride + idx);
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    *c = v;
+  }
+}
+

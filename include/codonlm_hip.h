@@ -127,8 +127,15 @@ typedef struct {
 typedef struct {
   int n, K, tile_m;
   cg_dw_product p[CG_DW_MAX];
+  /* ABI 0.3: ksplit > 1 (<= 8) splits every tile's token range over ksplit workgroups (more work
+   * items where a group's tiles do not fill the CUs); slices 1.. write fp32 slabs into workspace
+   * (ws_bytes >= cg_gemm_dw_grouped_workspace(grp), 16-B aligned, else CG_EINVAL) and one
+   * reduction launch adds them into C in slice order -- deterministic.  0 / 1 = no split. */
+  int ksplit;
+  float* workspace; size_t ws_bytes;
 } cg_dw_group;
 int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream);
+size_t cg_gemm_dw_grouped_workspace(const cg_dw_group* grp);
 /* tiles one product contributes at tile_m (0 = current default); default tile_m setter */
 int cg_gemm_dw_tiles(int tile_m, int N_out, int K_out);
 int cg_gemm_dw_set_tile(int tile_m);

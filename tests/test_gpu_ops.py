@@ -374,9 +374,10 @@ def test_attention_mfma_full_geometry(B, T, H, KV, hd, p):
         assert e <= 2e-2, (name, e)
 
 
+@pytest.mark.parametrize("ksplit", [1, 2, 3])
 @pytest.mark.parametrize("K", [2048, 1023, 37])
 @pytest.mark.parametrize("tile", [128, 129, 256, 512])
-def test_gemm_dw_grouped_tiles(tile, K):
+def test_gemm_dw_grouped_tiles(tile, K, ksplit):
     """Grouped full-reduction dW (cg_gemm_dw_grouped) for every tile code, against fp32 products
     of the same bf16 operands: ragged N_out / K_out (partial tiles), strided operands, alpha and
     accumulate, products of different shapes in one launch, and token counts K that are not a
@@ -396,11 +397,21 @@ def test_gemm_dw_grouped_tiles(tile, K):
         ref = alpha * (dy.float().t() @ x.float()) + (out.clone() if acc else 0)
         prods.append((dy, x, out, alpha, acc))
         refs.append(ref)
-    ops.gemm_dw_grouped(prods, tile_m=tile)
+    first = [p[2].clone() for p in prods]
+    ops.gemm_dw_grouped(prods, tile_m=tile, ksplit=ksplit)
     torch.cuda.synchronize()
     for (dy, x, out, _, _), ref in zip(prods, refs):
         err = ((out - ref).abs().max() / ref.abs().max()).item()
-        assert err <= 1e-5, (tile, tuple(out.shape), err)
+        assert err <= 1e-5, (tile, ksplit, tuple(out.shape), err)
+    if ksplit > 1:  # the split (slabs + in-order reduction) is deterministic: a rerun is bitwise equal
+        again = []
+        for (dy, x, out, alpha, acc), f in zip(prods, first):
+            o2 = f.clone()
+            again.append((dy, x, o2, alpha, acc))
+        ops.gemm_dw_grouped(again, tile_m=tile, ksplit=ksplit)
+        torch.cuda.synchronize()
+        for (_, _, o2, _, _), (_, _, out, _, _) in zip(again, prods):
+            assert torch.equal(o2, out)
 
 
 @pytest.mark.parametrize("B,T,H,KV,hd,p", [(2, 1024, 8, 8, 64, 0.1), (2, 200, 4, 2, 48, 0.0), (1, 130, 2, 1, 32, 0.1)])
