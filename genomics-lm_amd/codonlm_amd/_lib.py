@@ -120,7 +120,8 @@ class Model(C.Structure):
                 ("aux_ready", i32), ("head_grad_scale", f32), ("head_grad_scale_dev", vp), ("d_term_logits", vp),
                 ("ld_d_term", i64),
                 ("d_offset_logits", vp * 8), ("dw_done_layer", i32),
-                ("head_dw_off", i64), ("head_dw_alpha", f32), ("head_dw_accumulate", i32), ("head_dw_pending", i32)]
+                ("head_dw_off", i64), ("head_dw_alpha", f32), ("head_dw_accumulate", i32), ("head_dw_pending", i32),
+                ("reduce_pending", ReduceBatch)]
 
 
 # name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
@@ -136,6 +137,8 @@ SIGNATURES = {
     "cg_set_head_dw_defer": (i32, [i32]),
     "cg_set_dw_order": (i32, [i32]),
     "cg_set_dw_group": (i32, [i32]),
+    "cg_set_dw_ksplit": (i32, [i32]),
+    "cg_struct_bytes": (sz, [C.c_char_p]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),
     "cg_gemm_dw_grouped_workspace": (sz, [C.POINTER(DwGroup)]),

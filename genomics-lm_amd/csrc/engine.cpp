@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <algorithm>
+#include <string>
 #include <vector>
 #include "../../include/codonlm_hip.h"
 
@@ -66,10 +67,9 @@ static int dw_forced_bm() {
   static const int forced = [] { const char* e = getenv("CG_DW_BM"); return e ? atoi(e) : 0; }();
   return forced;
 }
-static int dw_forced_ks() {
-  static const int forced = [] { const char* e = getenv("CG_DW_KSPLIT"); return e ? atoi(e) : 0; }();
-  return forced;
-}
+// 0: the planner's token-range split; 1..3: forced (CG_DW_KSPLIT / cg_set_dw_ksplit, for A/B and tests)
+static int g_dw_ks = [] { const char* e = getenv("CG_DW_KSPLIT"); return e ? atoi(e) : 0; }();
+static int dw_forced_ks() { return g_dw_ks; }
 // weight elements of one block's dW products (the slab a token-range split writes per slice)
 static long long dw_block_elems(const Dims& D) {
   const long long d = D.d;
@@ -609,19 +609,9 @@ bool group_ends(const Dims& D, int l) {
 // Parameter / bias gradient reductions deferred to the end of a dW group: the LayerNorm
 // backward and the fused column-sum epilogues of a group's blocks leave partial rows in their
 // slots; one cg_reduce_columns launch per group turns them into gradients (per-layer reduce
-// launches were ~5 us each, mostly idle GPU).  Keyed by model; phase 0 starts a backward.
-std::vector<std::pair<const cg_model*, cg_reduce_batch>>& pending_all() {
-  static std::vector<std::pair<const cg_model*, cg_reduce_batch>> v;
-  return v;
-}
-cg_reduce_batch& pending(const cg_model* m) {
-  auto& v = pending_all();
-  for (auto& e : v)
-    if (e.first == m) return e.second;
-  v.emplace_back(m, cg_reduce_batch{});
-  v.back().second.n = 0;
-  return v.back().second;
-}
+// launches were ~5 us each, mostly idle GPU).  The batch lives in the model (its lifetime and
+// thread ownership follow the model's); phase 0 starts a backward.
+cg_reduce_batch& pending(const cg_model* m) { return const_cast<cg_model*>(m)->reduce_pending; }
 int defer_reduce(const cg_model* m, const float* part, long long ld, int nrows, int cols, float* dst, int accumulate,
                  void* stream) {
   cg_reduce_batch& b = pending(m);
@@ -696,6 +686,12 @@ extern "C" int cg_set_dw_order(int order) {
   g_dw_order = order ? 1 : 0;
   return prev;
 }
+extern "C" int cg_set_dw_ksplit(int ks) {
+  const int prev = g_dw_ks;
+  g_dw_ks = ks < 0 || ks > 3 ? 0 : ks;
+  return prev;
+}
+
 extern "C" int cg_set_dw_group(int blocks) {
   const int prev = g_dw_group;
   g_dw_group = blocks < 0 ? 0 : blocks;
@@ -1467,6 +1463,18 @@ extern "C" int cg_model_decode(cg_model* m, const int64_t* tok, int B, int pos, 
   g.c_dtype = CG_F32;
   CK(cg_gemm(&g, C.s));
   return CG_OK;
+}
+
+extern "C" size_t cg_struct_bytes(const char* name) {
+  if (!name) return 0;
+  const std::string n(name);
+#define CG_SZ(T) \
+  if (n == #T) return sizeof(T);
+  CG_SZ(cg_gemm_desc) CG_SZ(cg_dw_product) CG_SZ(cg_dw_group) CG_SZ(cg_reduce_job) CG_SZ(cg_reduce_batch)
+  CG_SZ(cg_transpose_item) CG_SZ(cg_transpose_batch) CG_SZ(cg_adamw_segment) CG_SZ(cg_model_cfg)
+  CG_SZ(cg_param_entry) CG_SZ(cg_model)
+#undef CG_SZ
+  return 0;
 }
 
 extern "C" const char* cg_version(void) { return "codonlm_hip 0.3 gfx950"; }

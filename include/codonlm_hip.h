@@ -436,6 +436,9 @@ typedef struct {
   float head_dw_alpha;
   int head_dw_accumulate;
   int head_dw_pending;
+  /* engine-private: the parameter / bias gradient column reductions deferred to the end of the
+   * current dW group (one cg_reduce_columns launch per group) */
+  cg_reduce_batch reduce_pending;
 } cg_model;
 
 /* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
@@ -529,9 +532,18 @@ int cg_set_rope_fused(int on);
 /* grouped dW plan controls (read when a backward starts; change them only between steps):
  * cg_set_dw_order 1 = the short remainder group last from the top (default; env CG_DW_ORDER),
  * 0 = first; cg_set_dw_group(n) forces n blocks per group (0 = planner's choice; env
- * CG_DW_GROUP).  Both return the previous setting. */
+ * CG_DW_GROUP); cg_set_dw_ksplit(k) forces a k-way token-range split of every group's tiles
+ * (1..3; 0 = planner's choice; env CG_DW_KSPLIT) -- set it before the model's first step at a
+ * (B, T), which sizes the slab workspace.  All return the previous setting. */
 int cg_set_dw_order(int order);
 int cg_set_dw_group(int blocks);
+int cg_set_dw_ksplit(int ks);
+
+/* sizeof the named ABI struct ("cg_gemm_desc", "cg_dw_product", "cg_dw_group", "cg_reduce_job",
+ * "cg_reduce_batch", "cg_transpose_item", "cg_transpose_batch", "cg_adamw_segment",
+ * "cg_model_cfg", "cg_param_entry", "cg_model"), 0 for another name: lets a binding that mirrors
+ * the layouts check them against the library it loaded. */
+size_t cg_struct_bytes(const char* name);
 
 /* "codonlm_hip <abi> gfx950".  ABI 0.2 (round 3): cg_gemm_desc.ws_bytes and the size_t
  * workspace-size argument after every workspace pointer.  ABI 0.3 (round 4): cg_model gained

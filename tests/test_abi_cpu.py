@@ -27,6 +27,21 @@ def test_library_exports_every_declared_symbol():
     assert _lib.lib.cg_version().decode().startswith("codonlm_hip")
 
 
+def test_ctypes_struct_mirrors_match_the_library():
+    """Every struct the ctypes binding mirrors has the size the loaded library was built with
+    (cg_struct_bytes), so a field added on one side only fails here, not as a misread argument."""
+    import ctypes
+    from codonlm_amd import _lib as L
+    mirrors = {"cg_gemm_desc": L.GemmDesc, "cg_dw_product": L.DwProduct, "cg_dw_group": L.DwGroup,
+               "cg_reduce_job": L.ReduceJob, "cg_reduce_batch": L.ReduceBatch,
+               "cg_transpose_item": L.TransposeItem, "cg_transpose_batch": L.TransposeBatch,
+               "cg_adamw_segment": L.AdamwSegment, "cg_model_cfg": L.ModelCfg,
+               "cg_param_entry": L.ParamEntry, "cg_model": L.Model}
+    for name, cls in mirrors.items():
+        assert L.lib.cg_struct_bytes(name.encode()) == ctypes.sizeof(cls), name
+    assert L.lib.cg_struct_bytes(b"nope") == 0
+
+
 def test_product_path_never_imports_oracle():
     pkg = ROOT / "genomics-lm_amd" / "codonlm_amd"
     for f in pkg.rglob("*.py"):

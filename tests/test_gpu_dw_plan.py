@@ -3,6 +3,8 @@
 * the tied head's weight gradient, deferred from backward phase 0 into the first grouped dW
   launch: deferral on vs off, and the phase-2 fallback of a partial phase sequence
   (phase 0 then phase 2, no dW group to take the product);
+* the token-range split of the grouped dW tiles (cg_set_dw_ksplit 2 / 3 against 1) at C2 geometry,
+  where the planner's own choice is a 3-way split;
 * the group plans priced by tools/bucket_replay.py (short group first / last, 4/4/4, 6/6) give
   the gradients of one block per launch, and fire every block's bucket hook exactly once.
 
@@ -135,3 +137,33 @@ def test_rope_fused_equals_table_passes(hd, dropout):
     assert gf.keys() == gu.keys()
     for k in gf:
         assert _rel(gf[k], gu[k]) < 3e-2, (k, _rel(gf[k], gu[k]))
+
+
+def test_dw_ksplit_gives_the_same_gradients():
+    """C2 geometry (d256, H4, T512 -- the planner splits its one 6-block group 3 ways): every
+    block's dW with the token range cut into 1, 2 or 3 slices (slices summed in order into the
+    fp32 gradient) -- the same products in another summation order."""
+    from codonlm_amd import TinyGPT, _lib as L
+    x, y = _batch(B=8, T=512, seed=9)
+
+    def run(ks):
+        old = L.lib.cg_set_dw_ksplit(ks)
+        try:
+            torch.manual_seed(13)
+            m = TinyGPT(68, 512, n_layer=6, n_head=4, n_embd=256, dropout=0.1, label_smoothing=0.05,
+                        compute_dtype="bf16", device=DEV)
+            m.train()
+            m.flat_grads().zero_()
+            _, loss = m(x, y)
+            loss.backward()
+            torch.cuda.synchronize()
+            return m.flat_grads().detach().clone()
+        finally:
+            L.lib.cg_set_dw_ksplit(old)
+
+    ref = run(1)
+    assert float(ref.abs().max()) > 0
+    for ks in (0, 2, 3):
+        g = run(ks)
+        assert _rel(g, ref) < 1e-6, (ks, _rel(g, ref))
+        assert torch.equal(g, run(ks)), ks  # deterministic: slabs reduced in slice order
