@@ -32,13 +32,20 @@
 #ifndef CG_LW_PF
 #define CG_LW_PF 0
 #endif
+// residual L2 prefetch (experiment): with the fp32-residual epilogue each loader also issues, per
+// stage, one 4-byte LDS-DMA read per lane (into a scratch slot nobody reads) touching one 128-B line
+// of the tile's residual block, so the first 4 k-steps of a tile pull its 1024 residual lines
+// toward the CU while the MFMAs run instead of in the epilogue's burst; 0 = off
+#ifndef CG_LW_RPF
+#define CG_LW_RPF 0
+#endif
 namespace bfl {
 constexpr int CWAVES = 8, LWAVES = 4, THREADS = 64 * (CWAVES + LWAVES);
 constexpr int A_PIECES = bfw::A_BYTES / 1024, B_PIECES = bfw::B_BYTES / 1024;  // 32, 16 per stage
 constexpr int LA = A_PIECES / LWAVES, LB = B_PIECES / LWAVES;                  // 8, 4 per loader
 constexpr int PER_STAGE = LA + LB;                                             // DMAs per loader per stage
 constexpr int PF_OPS = CG_LW_PF ? LA : 0;                                      // prefetch reads per stage
-constexpr int SMEM = bfp::SMEM + (CG_LW_PF ? LWAVES * 256 : 0);
+constexpr int SMEM = bfp::SMEM + (CG_LW_PF || CG_LW_RPF ? LWAVES * 256 : 0);
 }  // namespace bfl
 
 template <int EPI, int CT>
@@ -81,6 +88,9 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
     const int L = wave - bfl::CWAVES;
     const __amdgpu_buffer_rsrc_t ra = rsrc(p.A, ((long long)(p.M - 1) * p.lda + p.K) * 2);
     const __amdgpu_buffer_rsrc_t rb = rsrc(p.B, ((long long)((SWG ? 2 : 1) * p.N - 1) * p.ldb + p.K) * 2);
+    const __amdgpu_buffer_rsrc_t rres =
+        rsrc((EPI & CG_EPI_RESID) ? (const void*)p.resid : (const void*)p.A,
+             (EPI & CG_EPI_RESID) ? ((long long)(p.M - 1) * p.ldr + p.N) * 4 : 0);
     uint32_t va[bfl::LA], vb[bfl::LB];
 #pragma unroll
     for (int j = 0; j < bfl::LA; ++j) va[j] = bfw::src_off<true>((L + bfl::LWAVES * j) * 1024 + 16 * lane, p.lda);
@@ -146,12 +156,29 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
         for (int j = 0; j < bfl::LA; ++j)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (bfw::lds_ptr_t)scr, 4, po == OOR ? OOR : po + va[j], 0, 0, 0);
       }
+      if constexpr (CG_LW_RPF && (EPI & CG_EPI_RESID)) {
+        uint32_t ro = OOR;
+        if (g < S) {
+          const int k = g / nt, t = g - k * nt;
+          const int q = t * bfl::LWAVES + L;  // 64-line piece q of the tile's 1024 (256 rows x 4 lines)
+          if (q < 16) {
+            int m0, n0;
+            tile_org(k, m0, n0);
+            const int line = q * 64 + lane;
+            const int row = m0 + (line >> 2), col = n0 + (line & 3) * 32;
+            if (row < p.M && col < p.N) ro = (uint32_t)(((long long)row * p.ldr + col) * 4);
+          }
+        }
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rres, (bfw::lds_ptr_t)(smem + bfp::SMEM + L * 256), 4, ro, 0, 0, 0);
+      }
     };
+    // residual prefetch ops per stage (1 with the fp32-residual epilogue under CG_LW_RPF)
+    constexpr int RPF = (CG_LW_RPF && (EPI & CG_EPI_RESID)) ? 1 : 0;
     if constexpr (RP) rope_offsets(0);
     issue(0);
     issue(1);
     for (int g = 0; g < S; ++g) {
-      wait_vm<bfl::PER_STAGE + 2 * bfl::PF_OPS>();  // stage g landed; stage g+1 may still be in flight
+      wait_vm<bfl::PER_STAGE + 2 * bfl::PF_OPS + 2 * RPF>();  // stage g landed; stage g+1 may still be in flight
       __builtin_amdgcn_s_barrier();
       issue(g + 2);  // into the slot of stage g-1, whose reads retired before this barrier
     }
