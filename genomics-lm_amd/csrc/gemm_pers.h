@@ -120,6 +120,11 @@ __device__ __forceinline__ float dpp_sum16(float t) {
 #endif
 // timing-only diagnostic builds of the column-sum epilogue: 1 no DPP row sums, 2 no partial
 // stores (out-of-range offsets), 3 no accumulation
+// SwiGLU-backward epilogue operand loads in at most this many early pieces (0: all at the top of
+// the tile's last k-step)
+#ifndef CG_DSW_NP
+#define CG_DSW_NP 0
+#endif
 #ifndef CG_COLSUM_DIAG
 #define CG_COLSUM_DIAG 0
 #endif
@@ -710,11 +715,13 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
   if (CG_PERS_DIAG == 3 && wave >= 4) __builtin_amdgcn_s_barrier();
   if (CG_PERS_DIAG == 4 && wave >= 4) __builtin_amdgcn_s_setprio(1);
 #ifndef CG_PERS_NO_SPREAD
-  const int np = NL == 0 ? 0 : nt >= 7 ? 4 : nt >= 5 ? 2 : nt >= 4 ? 1 : 0;
+  int np = NL == 0 ? 0 : nt >= 7 ? 4 : nt >= 5 ? 2 : nt >= 4 ? 1 : 0;
 #else
-  const int np = 0;
+  int np = 0;
 #endif
-  if constexpr (NL == 0 || DSW) {  // DSW: 52 more VGPRs held over 5 steps spill (204 -> 256 + scratch)
+  if constexpr (DSW) np = np > CG_DSW_NP ? CG_DSW_NP : np;
+  // DSW: 52 more VGPRs held over 5 steps spill (204 -> 256 + scratch); CG_DSW_NP caps its pieces
+  if constexpr (NL == 0 || (DSW && CG_DSW_NP == 0)) {
     tiles(std::integral_constant<int, 0>{});
   } else {
     if (np == 4) tiles(std::integral_constant<int, 4>{});
