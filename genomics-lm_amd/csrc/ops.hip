@@ -93,6 +93,77 @@ __device__ __forceinline__ void stw(bf16_t* p, const float* v) {
   else *(uint32_t*)p = u[0];
 }
 
+// LayerNorm row prefetch (env CG_LN_PF, bit set; unset = by measurement): 1 = the backward keeps
+// two rows in flight per wave, 2 = the forward runs 4 rows per wave with the next row's x loaded
+// before the current row's reductions.  rocprofv3 per kernel (profiles/round4/ln_prefetch.txt):
+// backward 23.88 -> 23.7 us at d 512, 34.39 -> 34.05 at d 384; forward 15.09 -> 14.11 at d 384
+// (W = 2) but 10.24 -> 10.44 at d 512 (W = 4), so the default takes the prefetching forward for
+// W = 2 rows only.
+static int g_ln_pf = [] {
+  const char* e = getenv("CG_LN_PF");
+  return e ? atoi(e) : -1;
+}();
+static inline bool ln_pf_bwd() { return g_ln_pf < 0 || (g_ln_pf & 1); }
+static inline bool ln_pf_fwd(int W) { return g_ln_pf < 0 ? W == 2 : (g_ln_pf & 2) != 0; }
+
+// PF rows per wave of the prefetching forward
+constexpr int LN_FWD_RPW = 4;
+template <typename TO, int W, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_pf(const float* __restrict__ x, long long ldx,
+                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                 TO* __restrict__ y, long long ldy, float* __restrict__ mean,
+                                                 float* __restrict__ rstd, int rows, float eps) {
+  constexpr int cols = 64 * W * NV;
+  const int lane = threadIdx.x & 63;
+  const int r0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * LN_FWD_RPW;
+  if (r0 >= rows) return;
+  const int r1 = min(rows, r0 + LN_FWD_RPW);
+  float gm[NV][W], bt[NV][W], v[NV][W];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    ldw<W>(gamma + W * (lane + 64 * i), gm[i]);
+    ldw<W>(beta + W * (lane + 64 * i), bt[i]);
+    ldw<W>(x + (long long)r0 * ldx + W * (lane + 64 * i), v[i]);
+  }
+  for (int row = r0; row < r1; ++row) {
+    float nv[NV][W];
+    const int nr = min(row + 1, r1 - 1);  // the last row's reload is unused
+#pragma unroll
+    for (int i = 0; i < NV; ++i) ldw<W>(x + (long long)nr * ldx + W * (lane + 64 * i), nv[i]);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < W; ++j) s += v[i][j];
+    const float mu = wave_sum(s) * (1.0f / cols);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const float a = v[i][j] - mu;
+        q += a * a;
+      }
+    const float rs = rsqrtf(wave_sum(q) * (1.0f / cols) + eps);
+    TO* yr = y + (long long)row * ldy;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      float o[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) o[j] = (v[i][j] - mu) * rs * gm[i][j] + bt[i][j];
+      stw<W>(yr + W * (lane + 64 * i), o);
+    }
+    if (lane == 0) {
+      if (mean) mean[row] = mu;
+      if (rstd) rstd[row] = rs;
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+#pragma unroll
+      for (int j = 0; j < W; ++j) v[i][j] = nv[i][j];
+  }
+}
+
 template <typename TO, int W, int NV>
 __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, long long ldx,
                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -150,8 +221,14 @@ static inline int ln_width(int cols, const void* a, long long lda, const void* b
 template <typename TO>
 static bool ln_fwd_fast(int W, int cols, dim3 g, hipStream_t s, const float* x, long long ldx, const float* gamma,
                         const float* beta, TO* y, long long ldy, float* mean, float* rstd, int rows, float eps) {
-#define LNF(WW, N) \
-  case N: hipLaunchKernelGGL((ln_fwd_vec<TO, WW, N>), g, dim3(256), 0, s, x, ldx, gamma, beta, y, ldy, mean, rstd, rows, eps); return true;
+#define LNF(WW, N)                                                                                                  \
+  case N:                                                                                                          \
+    if (ln_pf_fwd(WW))                                                                                             \
+      hipLaunchKernelGGL((ln_fwd_pf<TO, WW, N>), dim3(cg_cdiv(rows, 4 * LN_FWD_RPW)), dim3(256), 0, s, x, ldx, gamma, \
+                         beta, y, ldy, mean, rstd, rows, eps);                                                        \
+    else                                                                                                           \
+      hipLaunchKernelGGL((ln_fwd_vec<TO, WW, N>), g, dim3(256), 0, s, x, ldx, gamma, beta, y, ldy, mean, rstd, rows, eps); \
+    return true;
   if (W == 4) {
     switch (cols / 256) { LNF(4, 1) LNF(4, 2) LNF(4, 3) LNF(4, 4) default: return false; }
   }
@@ -214,7 +291,9 @@ extern "C" size_t cg_layernorm_bwd_workspace(int rows, int cols, int want_col) {
 // dgamma/dbeta partials in registers, combined across the block's 4 waves in LDS (fixed order).
 // g_in may alias g_out (the engine accumulates the residual gradient in place): each row's g_in
 // values are read before that row's g_out is written, and no other row touches them.
-template <typename TD, typename TO, int W, int NV>
+// PF: the next row's dy / x / residual-gradient loads are issued before the current row's
+// reductions (two rows in flight per wave)
+template <typename TD, typename TO, int W, int NV, bool PF = false>
 __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, long long lddy, const float* __restrict__ x,
                                                   long long ldx, const float* __restrict__ mean,
                                                   const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -233,31 +312,44 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
 #pragma unroll
     for (int j = 0; j < W; ++j) dg[i][j] = db[i][j] = dc[i][j] = 0.f;
   }
-  for (int row = r_begin + wave; row < r_end; row += 4) {
-    const float mu = mean[row], rs = rstd[row];
-    const float* xr = x + (long long)row * ldx;
-    const TD* dyr = dy + (long long)row * lddy;
-    float xh[NV][W], gy[NV][W];
-    float s1 = 0.f, s2 = 0.f;
-    // the residual-gradient row is loaded with dy and x, before the two row reductions
-    const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
-    float g2[NV][W];
-    if (gi) {
+  // one row's operands: the residual-gradient row is loaded with dy and x, before the reductions
+  struct RowIn { float mu, rs, g2[NV][W], d[NV][W], xv[NV][W]; };
+  auto load_row = [&](int row, RowIn& in) __attribute__((always_inline)) {
+    in.mu = mean[row];
+    in.rs = rstd[row];
+    if (g_in) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) ldw<W>(gi + W * (lane + 64 * i), g2[i]);
+      for (int i = 0; i < NV; ++i) ldw<W>(g_in + (long long)row * cols + W * (lane + 64 * i), in.g2[i]);
     }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       const int c = W * (lane + 64 * i);
-      float d[W], xv[W];
-      ldw<W>(dyr + c, d);
-      ldw<W>(xr + c, xv);
+      ldw<W>(dy + (long long)row * lddy + c, in.d[i]);
+      ldw<W>(x + (long long)row * ldx + c, in.xv[i]);
+    }
+  };
+  RowIn cur;
+  if (PF && r_begin + wave < r_end) load_row(r_begin + wave, cur);
+  for (int row = r_begin + wave; row < r_end; row += 4) {
+    if constexpr (!PF) {
+      load_row(row, cur);
+    }
+    RowIn nxt;
+    if constexpr (PF) load_row(min(row + 4, r_end - 1), nxt);  // the last row's reload is unused
+    const float mu = cur.mu, rs = cur.rs;
+    const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
+    float xh[NV][W], gy[NV][W];
+    float s1 = 0.f, s2 = 0.f;
+    float (&g2)[NV][W] = cur.g2;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
 #pragma unroll
       for (int j = 0; j < W; ++j) {
-        xh[i][j] = (xv[j] - mu) * rs;
-        gy[i][j] = d[j] * gm[i][j];
-        dg[i][j] += d[j] * xh[i][j];
-        db[i][j] += d[j];
+        const float d = cur.d[i][j];
+        xh[i][j] = (cur.xv[i][j] - mu) * rs;
+        gy[i][j] = d * gm[i][j];
+        dg[i][j] += d * xh[i][j];
+        db[i][j] += d;
         s1 += gy[i][j];
         s2 += gy[i][j] * xh[i][j];
       }
@@ -290,6 +382,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
         for (int j = 0; j < W; ++j) dc[i][j] += o[j];  // column sum of the consumer's dY (its bias gradient)
       }
     }
+    if constexpr (PF) cur = nxt;
   }
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -309,7 +402,15 @@ static bool ln_bwd_fast(int W, int cols, int nblk, hipStream_t s, const TD* dy, 
                         long long ldx, const float* mean, const float* rstd, const float* gamma, const float* g_in,
                         float* g_out, TO* g_out_t, uint32_t seed, uint32_t thr, float dscale, float* partials,
                         int rows, int want_col) {
-#define LNB(WW, N) case N: hipLaunchKernelGGL((ln_bwd_vec<TD, TO, WW, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows, want_col); return true;
+#define LNB(WW, N)                                                                                                  \
+  case N:                                                                                                          \
+    if (ln_pf_bwd())                                                                                               \
+      hipLaunchKernelGGL((ln_bwd_vec<TD, TO, WW, N, true>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, \
+                         gamma, g_in, g_out, g_out_t, seed, thr, dscale, partials, rows, want_col);                   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((ln_bwd_vec<TD, TO, WW, N>), dim3(nblk), dim3(256), 0, s, dy, lddy, x, ldx, mean, rstd, gamma, \
+                         g_in, g_out, g_out_t, seed, thr, dscale, partials, rows, want_col);                          \
+    return true;
   if (W == 4) {
     switch (cols / 256) { LNB(4, 1) LNB(4, 2) LNB(4, 3) LNB(4, 4) default: return false; }
   }
