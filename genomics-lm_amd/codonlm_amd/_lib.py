@@ -121,7 +121,7 @@ class Model(C.Structure):
                 ("ld_d_term", i64),
                 ("d_offset_logits", vp * 8), ("dw_done_layer", i32),
                 ("head_dw_off", i64), ("head_dw_alpha", f32), ("head_dw_accumulate", i32), ("head_dw_pending", i32),
-                ("reduce_pending", ReduceBatch)]
+                ("reduce_pending", ReduceBatch), ("embed_done", i32)]
 
 
 # name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
@@ -138,6 +138,7 @@ SIGNATURES = {
     "cg_set_dw_order": (i32, [i32]),
     "cg_set_dw_group": (i32, [i32]),
     "cg_set_dw_ksplit": (i32, [i32]),
+    "cg_set_dw_overlap": (i32, [i32]),
     "cg_struct_bytes": (sz, [C.c_char_p]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),

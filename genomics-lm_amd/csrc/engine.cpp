@@ -707,6 +707,43 @@ extern "C" int cg_set_head_dw_defer(int on) {
   g_head_dw_defer = on ? 1 : 0;
   return prev;
 }
+// 1 (env CG_DW_OVERLAP): the last dW group of a backward (blocks ending at block 0) runs on a side
+// stream while the main stream finishes block 0's LayerNorm backward, the deferred reductions and
+// the embedding backward -- meant to fill the CUs the group's tiles leave idle (C4: 192 tiles of
+// the 2-block group on 256 CUs); the main stream joins it before phase 1 returns, so the group's
+// bucket is final when the caller sees dw_done_layer == 0.  Default 0: measured slower on every
+// config (C4 7.652 -> 7.709 ms, C5 5.778 -> 5.952, C2 3.020 -> 3.068; the persistent dW walker
+// loses CUs to the streaming kernels while they run, profiles/round4/dw_overlap_ab.txt).
+static int g_dw_overlap = [] {
+  const char* e = getenv("CG_DW_OVERLAP");
+  return e ? atoi(e) : 0;
+}();
+extern "C" int cg_set_dw_overlap(int on) {
+  const int prev = g_dw_overlap;
+  g_dw_overlap = on ? 1 : 0;
+  return prev;
+}
+namespace {
+// per-device side stream and fork / join events (created once, never destroyed)
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+SideStream* side_stream() {
+  static SideStream ss[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& x = ss[dev];
+  if (!x.s) {
+    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return x.s = nullptr, nullptr;
+    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess)
+      return nullptr;
+  }
+  return &x;
+}
+}  // namespace
+
 namespace {
 
 // The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
@@ -1124,6 +1161,24 @@ extern "C" int cg_model_aux_forward(cg_model* m, float* term_logits, long long l
   return CG_OK;
 }
 
+namespace {
+// the embedding backward (model_tiny_gpt.py:305-312): tok_emb (+ pos_emb) gradients from the
+// residual gradient A.g left by block 0's first LayerNorm backward
+int embed_backward(const Ctx& C, cg_model* m, uint32_t seed, float p, int accumulate) {
+  const Dims& D = C.D;
+  const Acts& A = C.A;
+  const int d = D.d;
+  // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
+  const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
+  CK(cg_embed_bwd(m->idx, A.g, G(C, C.Lo.tok), nullptr, C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p, acc_tok,
+                  A.embws, A.nb.embws, C.s));
+  if (C.Lo.pos >= 0)
+    CK(cg_embed_bwd(m->idx, A.g, nullptr, G(C, C.Lo.pos), C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
+                    accumulate, A.embws, A.nb.embws, C.s));
+  return CG_OK;
+}
+}  // namespace
+
 extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumulate, void* stream) {
   if (!m || !m->idx || !m->grads) return CG_EINVAL;
   Ctx C;
@@ -1138,6 +1193,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
 
   if (phase == 0) {
     pending(m).n = 0;  // a backward starts here: drop anything an abandoned one left
+    m->embed_done = 0;
     CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
     CK(fill_head2(C, hoff));
@@ -1249,8 +1305,20 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
     g = lin_dx(C, sl.dqkv, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
     CK(cg_gemm(&g, C.s));
-    // the group's weight gradients once its lowest block is done
-    if (group_ends(D, l)) {
+    // the group's weight gradients once its lowest block is done; the last group (l == 0) on the
+    // side stream, joined below (see g_dw_overlap)
+    SideStream* ss = (l == 0 && group_ends(D, l) && g_dw_overlap) ? side_stream() : nullptr;
+    // the tied head's deferred product in this group writes tok_emb's gradient: the embedding
+    // backward then stays behind the join
+    const bool embed_early = ss && !m->head_dw_pending;
+    if (ss) {
+      if (hipEventRecord(ss->fork, C.s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
+        return CG_ELAUNCH;
+      Ctx C2 = C;
+      C2.s = ss->s;
+      CK(flush_dw(C2, l + slot_of(D, l), l, accumulate));
+      if (hipEventRecord(ss->join, ss->s) != hipSuccess) return CG_ELAUNCH;
+    } else if (group_ends(D, l)) {
       CK(flush_dw(C, l + slot_of(D, l), l, accumulate));
       m->dw_done_layer = l;
     }
@@ -1263,6 +1331,14 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // the group's parameter-gradient reductions (its LayerNorms, fused biases) in one launch,
     // before the caller starts the group's bucket all-reduce
     if (group_ends(D, l)) CK(flush_reduce(m, C.s));
+    if (ss) {
+      if (embed_early) {
+        CK(embed_backward(C, m, seed, p, accumulate));
+        m->embed_done = 1;
+      }
+      if (hipStreamWaitEvent(C.s, ss->join, 0) != hipSuccess) return CG_ELAUNCH;
+      m->dw_done_layer = l;
+    }
     return CG_OK;
   }
   if (phase == 2) {
@@ -1271,13 +1347,8 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       m->head_dw_pending = 0;
       CK(head_dw_now(C, m->head_dw_off, m->head_dw_alpha, m->head_dw_accumulate));
     }
-    // tied tok_emb already holds the head contribution from phase 0 -> always accumulate
-    const int acc_tok = m->cfg.tie_embeddings ? 1 : accumulate;
-    CK(cg_embed_bwd(m->idx, A.g, G(C, C.Lo.tok), nullptr, C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
-                    acc_tok, A.embws, A.nb.embws, C.s));
-    if (C.Lo.pos >= 0)
-      CK(cg_embed_bwd(m->idx, A.g, nullptr, G(C, C.Lo.pos), C.B, C.T, D.V, d, site_seed(seed, -1, SITE_EMB), p,
-                      accumulate, A.embws, A.nb.embws, C.s));
+    if (!m->embed_done) CK(embed_backward(C, m, seed, p, accumulate));
+    m->embed_done = 0;
     return CG_OK;
   }
   return CG_EINVAL;

@@ -439,6 +439,9 @@ typedef struct {
   /* engine-private: the parameter / bias gradient column reductions deferred to the end of the
    * current dW group (one cg_reduce_columns launch per group) */
   cg_reduce_batch reduce_pending;
+  /* engine-private: the embedding backward already ran inside phase 1 of block 0 (overlapped
+   * with the last dW group), so phase 2 skips it */
+  int embed_done;
 } cg_model;
 
 /* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
@@ -538,6 +541,11 @@ int cg_set_rope_fused(int on);
 int cg_set_dw_order(int order);
 int cg_set_dw_group(int blocks);
 int cg_set_dw_ksplit(int ks);
+/* 1 (env CG_DW_OVERLAP): the last dW group of a backward runs on a per-device side stream beside
+ * block 0's LayerNorm backward, the deferred reductions and the embedding backward, joined before
+ * phase 1 of block 0 returns; 0 (default, measured faster) = all on the caller's stream.  Returns
+ * the previous setting. */
+int cg_set_dw_overlap(int on);
 
 /* sizeof the named ABI struct ("cg_gemm_desc", "cg_dw_product", "cg_dw_group", "cg_reduce_job",
  * "cg_reduce_batch", "cg_transpose_item", "cg_transpose_batch", "cg_adamw_segment",

@@ -167,3 +167,37 @@ def test_dw_ksplit_gives_the_same_gradients():
         g = run(ks)
         assert _rel(g, ref) < 1e-6, (ks, _rel(g, ref))
         assert torch.equal(g, run(ks)), ks  # deterministic: slabs reduced in slice order
+
+
+@pytest.mark.parametrize("n_layer,tie,dropout", [(12, True, 0.1), (3, True, 0.0), (5, False, 0.1)])
+def test_dw_overlap_gives_the_same_gradients(n_layer, tie, dropout):
+    """The last dW group on the side stream beside block 0's LayerNorm backward, the deferred
+    reductions and the embedding backward (cg_set_dw_overlap(1), an A/B switch, off by default)
+    against everything on one stream: the same kernels on the same operands, so every gradient is bitwise equal.
+    n_layer 3 is one group that also carries the tied head's deferred product (the embedding
+    backward then stays behind the join); 12 ends on a short group; 5 is untied."""
+    from codonlm_amd import TinyGPT, _lib as L
+    x, y = _batch()
+
+    def run(on):
+        old = L.lib.cg_set_dw_overlap(int(on))
+        try:
+            torch.manual_seed(21)
+            m = TinyGPT(68, 128, n_layer=n_layer, n_head=4, n_embd=128, dropout=dropout, tie_embeddings=tie,
+                        label_smoothing=0.05, compute_dtype="bf16", device=DEV)
+            m.train()
+            fired = []
+            m._bucket_hook = fired.append
+            m.flat_grads().zero_()
+            _, loss = m(x, y)
+            loss.backward()
+            torch.cuda.synchronize()
+            return m.flat_grads().detach().clone(), fired
+        finally:
+            L.lib.cg_set_dw_overlap(old)
+
+    g1, f1 = run(True)
+    g0, f0 = run(False)
+    assert float(g0.abs().max()) > 0
+    assert sorted(map(str, f1)) == sorted(map(str, f0))
+    assert torch.equal(g1, g0)
