@@ -30,6 +30,18 @@
 // SIMD's other wave fills the gaps with VALU work instead of delaying them (A/B variant)
 // dK/dV body order (experiment): 0 = per 32-query half S, dP -> softmax / dS -> dV, dK; 1 = both
 // halves' S and dP first, so one half's VALU runs under the other half's MFMAs in the same wave
+// ATTN_DKDV_STATIC: the dK/dV body instantiated twice, for full and partial tiles (a straight-line
+// fast path the scheduler sees whole); ATTN_DKDV_SGB: with ATTN_DKDV_PIPE, sched_group_barrier
+// hints interleaving each MFMA run with the other half's VALU (1 MFMA : N VALU)
+#ifndef ATTN_DKDV_STATIC
+#define ATTN_DKDV_STATIC 0
+#endif
+#ifndef ATTN_DQ_STATIC
+#define ATTN_DQ_STATIC 0
+#endif
+#ifndef ATTN_DKDV_SGB
+#define ATTN_DKDV_SGB 0
+#endif
 #ifndef ATTN_DKDV_PIPE
 #define ATTN_DKDV_PIPE 0
 #endif
@@ -776,7 +788,10 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
     // set to -inf before the exponent; the branch touches only s, so the dQ accumulators keep
     // their registers across it (a branch around the whole body made hipcc copy them back at
     // the join)
-    auto body = [&](bool full) __attribute__((always_inline)) {
+    auto body = [&](auto full_c) __attribute__((always_inline)) {
+      bool full;
+      if constexpr (std::is_same_v<decltype(full_c), bool>) full = full_c;
+      else full = decltype(full_c)::value;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         ATTN_SETPRIO(1);
@@ -829,7 +844,15 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
         ATTN_SETPRIO(0);
       }
     };
-    if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) body((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max));
+    if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
+      const bool full = (k0 + KT - 1 <= q0w) && (k0 >= w_lo_max);
+      if constexpr (ATTN_DQ_STATIC) {
+        if (full) body(std::true_type{});
+        else body(std::false_type{});
+      } else {
+        body(full);
+      }
+    }
     if (!ATTN_DIAG_NODRAIN) dma_drain();  // diagnostic builds only (results invalid)
     __syncthreads();
   };
@@ -1031,8 +1054,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       }
       ATTN_SETPRIO(0);
     };
-    auto phase_ds = [&](int qb, bool full, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1, v8bf& sb0,
+    auto phase_ds = [&](int qb, auto full_c, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1, v8bf& sb0,
                         v8bf& sb1) __attribute__((always_inline)) {
+      bool full;
+      if constexpr (std::is_same_v<decltype(full_c), bool>) full = full_c;
+      else full = decltype(full_c)::value;
       if (!full) {
 #pragma unroll
         for (int rg = 0; rg < 16; rg += 4) {
@@ -1096,15 +1122,31 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       }
       ATTN_SETPRIO(0);
     };
-    auto body = [&](bool full) __attribute__((always_inline)) {
+    auto body = [&](auto full) __attribute__((always_inline)) {
       if constexpr (ATTN_DKDV_PIPE) {
         v16f s0, dp0, nd0, s1, dp1, nd1;
         v8bf a0, a1, a2, a3, b0, b1, b2, b3;
         phase_sdp(0, s0, dp0, nd0);
         phase_sdp(1, s1, dp1, nd1);
         phase_ds(0, full, s0, dp0, nd0, a0, a1, a2, a3);
+        if constexpr (ATTN_DKDV_SGB > 0) {
+          // half 1's S / dP MFMAs among half 0's softmax / keep / pack VALU
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DKDV_SGB, 0);
+          }
+        }
         phase_dkdv(0, a0, a1, a2, a3);
         phase_ds(1, full, s1, dp1, nd1, b0, b1, b2, b3);
+        if constexpr (ATTN_DKDV_SGB > 0) {
+          // half 0's dV / dK MFMAs among half 1's VALU
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DKDV_SGB, 1);
+          }
+        }
         phase_dkdv(1, b0, b1, b2, b3);
       } else {
 #pragma unroll
@@ -1117,7 +1159,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         }
       }
     };
-    if (active) body((q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0));
+    if (active) {
+      const bool full = (q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0);
+      if constexpr (ATTN_DKDV_STATIC) {
+        if (full) body(std::true_type{});
+        else body(std::false_type{});
+      } else {
+        body(full);
+      }
+    }
     if (more1) {  // n1's data (issued an iteration ago) landed; n2's DMAs may still be in flight
       if (more2) dma_wait<NV>();
       else dma_wait<0>();
