@@ -36,8 +36,10 @@
 #ifndef ATTN_DKDV_STATIC
 #define ATTN_DKDV_STATIC 0
 #endif
+// ATTN_DQ_STATIC (default 1): the dQ body likewise; measured 53.1-53.4 -> 49.8-50.3 us per C4 launch
+// (profiles/round4/attn_static_ab.txt), while the dK/dV one is not faster (72.0 -> 72.3) and stays off
 #ifndef ATTN_DQ_STATIC
-#define ATTN_DQ_STATIC 0
+#define ATTN_DQ_STATIC 1
 #endif
 #ifndef ATTN_DKDV_SGB
 #define ATTN_DKDV_SGB 0
