@@ -22,6 +22,8 @@ EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_DROPOUT, EPI_ACCUM, EPI_COLSUM = 1
 EPI_SWIGLU, EPI_DSWIGLU = 128, 256
 EPI_GELU_DERIV = 512  # GELU: aux_out = gelu'(v); DGELU: aux holds gelu' (out = v * aux)
 EPI_ROPE = 1024  # rotate-half RoPE of the q / k head columns after the bias (loader-wave tile only)
+# cg_gemm_desc.tile: automatic, or one bf16 kernel forced (tests / A/B runs)
+TILE_AUTO, TILE_VEC, TILE_WIDE, TILE_PERS, TILE_PERS_LW = range(5)
 (PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV,
  PROBE_GEMM_DW_GROUPED, PROBE_GEMM_PERS) = range(9)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
@@ -32,11 +34,9 @@ PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", P
 # starts with the prefix belongs to the class; bench.py / tools/kstats.py sum them)
 PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: ("gemm_dw_kernel",), PROBE_ATTN_FWD: ("attn_fwd_mfma",),
                  PROBE_ATTN_DQ: ("attn_bwd_dq_mfma",), PROBE_ATTN_DKDV: ("attn_bwd_dkdv_mfma",),
-                 # the persistent forward / dX class: the eight-wave kernel, its loader-wave variant
-                 # (plain and bias-only products) and the ping-pong variants (gemm_pp.h, gemm_pp2.h;
-                 # off by default), all launched through cg_gemm's persistent path, probed together
-                 PROBE_GEMM_PERS: ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel", "gemm_bf16_pp_kernel",
-                                   "gemm_bf16_pp2_kernel")}
+                 # the persistent forward / dX class: the eight-wave kernel and its loader-wave
+                 # variant, both launched through cg_gemm's persistent path, probed together
+                 PROBE_GEMM_PERS: ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel")}
 
 # parameter kinds (enum in the header)
 (P_TOK_EMB, P_POS_EMB, P_LN1_W, P_LN1_B, P_Q_W, P_K_W, P_V_W, P_Q_B, P_K_B, P_V_B, P_PROJ_W,
@@ -56,7 +56,8 @@ class GemmDesc(C.Structure):
                 ("aux", vp), ("aux_out", vp), ("ld_aux", i64),
                 ("drop_seed", u32), ("drop_p", f32), ("split_k", i32), ("workspace", vp),
                 ("n_valid", i32), ("ws_bytes", sz),
-                ("rope_cos", vp), ("rope_sin", vp), ("rope_T", i32), ("rope_hd", i32), ("rope_heads", i32)]
+                ("rope_cos", vp), ("rope_sin", vp), ("rope_T", i32), ("rope_hd", i32), ("rope_heads", i32),
+                ("tile", i32), ("max_wg", i32)]
 
 
 DW_MAX = 32
@@ -69,7 +70,7 @@ class DwProduct(C.Structure):
 
 class DwGroup(C.Structure):
     _fields_ = [("n", i32), ("K", i32), ("tile_m", i32), ("p", DwProduct * DW_MAX),
-                ("ksplit", i32), ("workspace", vp), ("ws_bytes", sz)]
+                ("ksplit", i32), ("workspace", vp), ("ws_bytes", sz), ("max_wg", i32)]
 
 
 REDUCE_MAX = 48
@@ -99,12 +100,18 @@ class TransposeBatch(C.Structure):
     _fields_ = [("n", i32), ("items", TransposeItem * TRANSPOSE_MAX)]
 
 
+class ModelOpts(C.Structure):
+    """cg_model_opts: all zero = the measured defaults"""
+    _fields_ = [("dw_group", i32), ("dw_ksplit", i32), ("dw_remainder_first", i32), ("head_dw_separate", i32),
+                ("rope_tables", i32), ("attn_mask_kernel", i32), ("dw_plan_tokens", i32)]
+
+
 class ModelCfg(C.Structure):
     _fields_ = [("vocab_size", i32), ("block_size", i32), ("n_layer", i32), ("n_head", i32),
                 ("n_kv_head", i32), ("n_embd", i32), ("use_swiglu", i32), ("use_rope", i32),
                 ("sep_id", i32), ("tie_embeddings", i32), ("termination_aux", i32),
                 ("termination_n_classes", i32), ("n_offsets", i32), ("offsets", i32 * 8),
-                ("dropout", f32), ("label_smoothing", f32), ("ln_eps", f32), ("dtype", i32)]
+                ("dropout", f32), ("label_smoothing", f32), ("ln_eps", f32), ("dtype", i32), ("opts", ModelOpts)]
 
 
 class ParamEntry(C.Structure):
@@ -121,31 +128,18 @@ class Model(C.Structure):
                 ("ld_d_term", i64),
                 ("d_offset_logits", vp * 8), ("dw_done_layer", i32),
                 ("head_dw_off", i64), ("head_dw_alpha", f32), ("head_dw_accumulate", i32), ("head_dw_pending", i32),
-                ("reduce_pending", ReduceBatch), ("embed_done", i32)]
+                ("reduce_pending", ReduceBatch)]
 
 
 # name -> (restype, argtypes) for every symbol include/codonlm_hip.h declares
 SIGNATURES = {
     "cg_gemm": (i32, [C.POINTER(GemmDesc), vp]),
-    "cg_gemm_set_wide": (i32, [i32]),
-    "cg_gemm_set_pers": (i32, [i32]),
-    "cg_set_cu_reserve": (i32, [i32]),
-    "cg_gemm_set_pers_lw": (i32, [i32]),
-    "cg_gemm_set_pers_pp": (i32, [i32]),
-    "cg_gemm_set_pers_pp2": (i32, [i32]),
-    "cg_set_rope_fused": (i32, [i32]),
-    "cg_set_head_dw_defer": (i32, [i32]),
-    "cg_set_dw_order": (i32, [i32]),
-    "cg_set_dw_group": (i32, [i32]),
-    "cg_set_dw_ksplit": (i32, [i32]),
-    "cg_set_dw_overlap": (i32, [i32]),
     "cg_struct_bytes": (sz, [C.c_char_p]),
     "cg_pers_cus": (i32, []),
     "cg_diag_occupy": (i32, [i32, i32, vp]),
     "cg_gemm_dw_grouped_workspace": (sz, [C.POINTER(DwGroup)]),
     "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),
     "cg_gemm_dw_tiles": (i32, [i32, i32, i32]),
-    "cg_gemm_dw_set_tile": (i32, [i32]),
     "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
     "cg_layernorm_bwd_blocks": (i32, [i32]),
     "cg_layernorm_bwd_workspace": (sz, [i32, i32, i32]),
@@ -191,7 +185,7 @@ SIGNATURES = {
     "cg_nonfinite_flag": (i32, [vp, i64, vp, vp]),
     "cg_model_param_layout": (i32, [C.POINTER(ModelCfg), C.POINTER(ParamEntry), i32, C.POINTER(i64)]),
     "cg_model_workspace_bytes": (sz, [C.POINTER(ModelCfg), i32, i32]),
-    "cg_model_dw_plan": (i32, [C.POINTER(ModelCfg), C.POINTER(i32), C.POINTER(i32)]),
+    "cg_model_dw_plan": (i32, [C.POINTER(ModelCfg), i32, i32, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]),
     "cg_model_forward": (i32, [C.POINTER(Model), vp, vp, i32, i32, i32, u32, i32, vp, vp, vp]),
     "cg_model_aux_forward": (i32, [C.POINTER(Model), vp, i64, C.POINTER(vp), i64, vp]),
     "cg_model_backward": (i32, [C.POINTER(Model), i32, i32, i32, vp]),

@@ -38,6 +38,8 @@ class EngineConfig:
     label_smoothing: float = 0.0
     ln_eps: float = 1e-5
     dtype: str = "fp32"  # "fp32" (parity) | "bf16" (throughput)
+    # cg_model_opts fields as ((name, value), ...): measured engine alternatives (tests, A/B runs)
+    opts: tuple = ()
 
     @property
     def head_dim(self) -> int:
@@ -66,6 +68,11 @@ class EngineConfig:
         c.label_smoothing = float(self.label_smoothing)
         c.ln_eps = float(self.ln_eps)
         c.dtype = L.CG_BF16 if self.dtype == "bf16" else L.CG_F32
+        known = {f for f, _ in L.ModelOpts._fields_}
+        for k, v in self.opts:
+            if k not in known:
+                raise ValueError(f"unknown engine option {k!r} (cg_model_opts: {sorted(known)})")
+            setattr(c.opts, k, int(v))
         return c
 
 

@@ -13,7 +13,9 @@ engine's backward and leaves the gradients in the flat grad buffer, which every
 ``param.grad`` views.
 
 Extra keyword arguments (not in the reference): ``compute_dtype`` ("fp32" parity mode,
-"bf16" throughput mode with fp32 master weights) and ``device``.
+"bf16" throughput mode with fp32 master weights), ``device`` and ``engine_opts`` (a dict of
+cg_model_opts fields selecting measured engine alternatives for tests / A/B runs; empty = the
+defaults).
 """
 from __future__ import annotations
 
@@ -199,7 +201,7 @@ class TinyGPT(nn.Module):
                  n_kv_head: int | None = None, use_sdpa: bool = False, loss_weights=None,
                  termination_aux: bool = False, termination_n_classes: int = 5, multi_offset_targets=None,
                  use_swiglu: bool = False, use_rope: bool = False, use_shape_guidance: bool = False, *,
-                 compute_dtype: str = "fp32", device=None):
+                 compute_dtype: str = "fp32", device=None, engine_opts: dict | None = None):
         super().__init__()
         if use_shape_guidance:
             raise ValueError("use_shape_guidance is outside the MI355X hot path (SURVEY §2: biophysics encoder)")
@@ -255,7 +257,8 @@ class TinyGPT(nn.Module):
                                   termination_aux=self.termination_aux,
                                   termination_n_classes=self.termination_n_classes,
                                   multi_offset_targets=tuple(self.multi_offset_targets), dropout=self.dropout_p,
-                                  label_smoothing=self.label_smoothing, dtype=compute_dtype)
+                                  label_smoothing=self.label_smoothing, dtype=compute_dtype,
+                                  opts=tuple(sorted((engine_opts or {}).items())))
         self._layout, total = param_layout(self._ecfg)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cpu"

@@ -28,11 +28,12 @@ def _p(t):
 
 def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=None, out_dtype=None,
          bias=None, resid=None, epilogue=0, aux=None, aux_out=None, alpha=1.0, drop_seed=0, drop_p=0.0,
-         split_k=1, colsum_out=None, n_valid=0, rope=None):
+         split_k=1, colsum_out=None, n_valid=0, rope=None, tile=0, max_wg=0):
     """C[m,n] = epi(alpha * sum_k A(m,k) B(n,k)); A(m,k)=a[m,k] if a_kcontig else a[k,m]; same for B.
     colsum_out (fp32 [N]): also the column sums of C (CG_EPI_COLSUM partials + cg_colsum_reduce).
     rope = (cos, sin, T, hd, heads): CG_EPI_ROPE -- the first heads*hd columns rotated at position
-    m % T after the bias (tables fp32 [>= T][hd/2])."""
+    m % T after the bias (tables fp32 [>= T][hd/2]).  tile: L.TILE_* (0 = automatic); max_wg: cap
+    on the persistent grid (0 = one workgroup per CU)."""
     for t in (a, b):
         L.require_device(t, "gemm")
     if a.dtype != b.dtype:
@@ -72,6 +73,7 @@ def gemm(a, b, *, a_kcontig=True, b_kcontig=True, M=None, N=None, K=None, out=No
     d.split_k, d.workspace = int(split_k), _p(ws)
     d.ws_bytes = 0 if ws is None else ws.numel() * ws.element_size()
     d.n_valid = int(n_valid)
+    d.tile, d.max_wg = int(tile), int(max_wg)
     if rope is not None:
         cos, sin, rT, rhd, rheads = rope
         d.epilogue |= L.EPI_ROPE

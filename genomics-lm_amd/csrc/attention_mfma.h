@@ -17,48 +17,13 @@
 #pragma once
 #include <type_traits>
 
-#ifndef ATTN_FWD_WPS
+// waves per SIMD the forward and dQ kernels are register-limited to (dQ at 3, <= 168 VGPRs, spilled
+// once S and dP were seeded by MFMAs; 2 measured 3-5 % faster on the C4 backward)
 #define ATTN_FWD_WPS 2
-#endif
-#ifndef ATTN_DQ_WPS
-// waves per SIMD the dQ kernel is register-limited to: 3 (<= 168 VGPRs) spilled once S and dP were
-// seeded by MFMAs; 2 measured 3-5 % faster on the C4 backward (tools/attn_time.py, same box)
 #define ATTN_DQ_WPS 2
-#endif
-
-// ATTN_PRIO: raise a wave's issue priority while it issues its MFMA chains (s_setprio), so the
-// SIMD's other wave fills the gaps with VALU work instead of delaying them (A/B variant)
-// dK/dV body order (experiment): 0 = per 32-query half S, dP -> softmax / dS -> dV, dK; 1 = both
-// halves' S and dP first, so one half's VALU runs under the other half's MFMAs in the same wave
-// ATTN_DKDV_STATIC: the dK/dV body instantiated twice, for full and partial tiles (a straight-line
-// fast path the scheduler sees whole); ATTN_DKDV_SGB: with ATTN_DKDV_PIPE, sched_group_barrier
-// hints interleaving each MFMA run with the other half's VALU (1 MFMA : N VALU)
-#ifndef ATTN_DKDV_STATIC
-#define ATTN_DKDV_STATIC 0
-#endif
-// ATTN_DQ_STATIC (default 1): the dQ body likewise; measured 53.1-53.4 -> 49.8-50.3 us per C4 launch
-// (profiles/round4/attn_static_ab.txt), while the dK/dV one is not faster (72.0 -> 72.3) and stays off
-#ifndef ATTN_DQ_STATIC
-#define ATTN_DQ_STATIC 1
-#endif
-#ifndef ATTN_DKDV_SGB
-#define ATTN_DKDV_SGB 0
-#endif
-#ifndef ATTN_DKDV_PIPE
-#define ATTN_DKDV_PIPE 0
-#endif
-#ifndef ATTN_PRIO
-#define ATTN_PRIO 0
-#endif
-// timing-only diagnostic: the forward and dQ kernels skip the per-tile DMA drain
-#ifndef ATTN_DIAG_NODRAIN
-#define ATTN_DIAG_NODRAIN 0
-#endif
-#if ATTN_PRIO
-#define ATTN_SETPRIO(x) __builtin_amdgcn_s_setprio(x)
-#else
-#define ATTN_SETPRIO(x) ((void)0)
-#endif
+// Measured and removed (rounds 2-4): s_setprio around the MFMA chains; the dK/dV
+// halves' S / dP issued before either half's softmax (with or without sched_group_barrier
+// hints); a full / partial-tile split of the dK/dV body (the dQ body keeps it: 53 -> 50 us).
 
 namespace fa {
 constexpr int HDP = 64;        // padded head dim held in LDS / registers
@@ -597,18 +562,15 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
                           ((wl & 0x00C000C0u) << 6);
       wout = sp << (2 * hl);
     }
-    ATTN_SETPRIO(1);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 0), pa, o0, 0, 0, 0);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 0), pb, o0, 0, 0, 0);
     if constexpr (hd > 32) {
       o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 1), pa, o1, 0, 0, 0);
       o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 1), pb, o1, 0, 0, 0);
     }
-    ATTN_SETPRIO(0);
   };
   auto body = [&](const char* Ki, const char* Vi, int k0, uint2 wc, auto full_c) __attribute__((always_inline)) {
     v16f s0 = zero16(), s1 = zero16();
-    ATTN_SETPRIO(1);
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks)
       if (ks < nks) s0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, 0, ks), qf[ks], s0, 0, 0, 0);
@@ -617,7 +579,6 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
     for (int ks = 0; ks < 4; ++ks)
       if (ks < nks) s1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Ki, ro, 32, ks), qf[ks], s1, 0, 0, 0);
     __builtin_amdgcn_sched_barrier(0);
-    ATTN_SETPRIO(0);
     // S feeds inline asm (max3): hipcc pads the XDL-result -> VALU-read hazard only before its own
     // instructions, so each half's accumulator passes through a wait of 19 states first (>= the
     // 16-pass rule); without it v_max3 can read a stale accumulator and the row max varies run to run
@@ -654,7 +615,7 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       if ((k0 + KT - 1 <= q0w) && (k0 >= w_lo_max)) body(Ki, Vi, k0, wc, std::true_type{});
       else body(Ki, Vi, k0, wc, std::false_type{});
     }
-    if (!ATTN_DIAG_NODRAIN) dma_drain();  // diagnostic builds only (results invalid)
+    dma_drain();
     __syncthreads();
   };
   for (int t = t0; t <= t1; t += 2) {
@@ -796,7 +757,6 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
       else full = decltype(full_c)::value;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        ATTN_SETPRIO(1);
         v16f s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, lsefrag, zero16(), 0, 0, 0);
         v16f dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(onesk, ndfrag, zero16(), 0, 0, 0);
 #pragma unroll
@@ -806,7 +766,6 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Vi, ro, kb * 32, ks), df[ks], dp, 0, 0, 0);
           }
         }
-        ATTN_SETPRIO(0);
         const int kq = myq - k0 - kb * 32, kl = lo - k0 - kb * 32;
         if (!full) {
 #pragma unroll
@@ -836,26 +795,20 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
           }
         }
         const v8bf b0 = pack_b(s, 0), b1 = pack_b(s, 1);
-        ATTN_SETPRIO(1);
         a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 0), b0, a0, 0, 0, 0);
         a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 0), b1, a0, 0, 0, 0);
         if constexpr (hd > 32) {
           a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 1), b0, a1, 0, 0, 0);
           a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 1), b1, a1, 0, 0, 0);
         }
-        ATTN_SETPRIO(0);
       }
     };
     if (k0 <= w_qmax && k0 + KT - 1 >= w_lo_min) {
       const bool full = (k0 + KT - 1 <= q0w) && (k0 >= w_lo_max);
-      if constexpr (ATTN_DQ_STATIC) {
-        if (full) body(std::true_type{});
-        else body(std::false_type{});
-      } else {
-        body(full);
-      }
+      if (full) body(std::true_type{});
+      else body(std::false_type{});
     }
-    if (!ATTN_DIAG_NODRAIN) dma_drain();  // diagnostic builds only (results invalid)
+    dma_drain();
     __syncthreads();
   };
   for (int t = t0; t <= t1; t += 2) {
@@ -1046,7 +999,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
       }
       dp = nd;
-      ATTN_SETPRIO(1);
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         if (ks < nks) {
@@ -1054,7 +1006,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
           dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
         }
       }
-      ATTN_SETPRIO(0);
     };
     auto phase_ds = [&](int qb, auto full_c, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1, v8bf& sb0,
                         v8bf& sb1) __attribute__((always_inline)) {
@@ -1111,7 +1062,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
     };
     auto phase_dkdv = [&](int qb, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
                           __attribute__((always_inline)) {
-      ATTN_SETPRIO(1);
       dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 0), pb0, dv0, 0, 0, 0);
       dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 0), pb1, dv0, 0, 0, 0);
       dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 0), sb0, dk0, 0, 0, 0);
@@ -1122,53 +1072,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
         dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 1), sb0, dk1, 0, 0, 0);
         dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 1), sb1, dk1, 0, 0, 0);
       }
-      ATTN_SETPRIO(0);
     };
     auto body = [&](auto full) __attribute__((always_inline)) {
-      if constexpr (ATTN_DKDV_PIPE) {
-        v16f s0, dp0, nd0, s1, dp1, nd1;
-        v8bf a0, a1, a2, a3, b0, b1, b2, b3;
-        phase_sdp(0, s0, dp0, nd0);
-        phase_sdp(1, s1, dp1, nd1);
-        phase_ds(0, full, s0, dp0, nd0, a0, a1, a2, a3);
-        if constexpr (ATTN_DKDV_SGB > 0) {
-          // half 1's S / dP MFMAs among half 0's softmax / keep / pack VALU
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DKDV_SGB, 0);
-          }
-        }
-        phase_dkdv(0, a0, a1, a2, a3);
-        phase_ds(1, full, s1, dp1, nd1, b0, b1, b2, b3);
-        if constexpr (ATTN_DKDV_SGB > 0) {
-          // half 0's dV / dK MFMAs among half 1's VALU
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-            __builtin_amdgcn_sched_group_barrier(0x002, ATTN_DKDV_SGB, 1);
-          }
-        }
-        phase_dkdv(1, b0, b1, b2, b3);
-      } else {
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          v16f s, dp, nd;
-          v8bf x0, x1, x2, x3;
-          phase_sdp(qb, s, dp, nd);
-          phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
-          phase_dkdv(qb, x0, x1, x2, x3);
-        }
+      for (int qb = 0; qb < 2; ++qb) {
+        v16f s, dp, nd;
+        v8bf x0, x1, x2, x3;
+        phase_sdp(qb, s, dp, nd);
+        phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
+        phase_dkdv(qb, x0, x1, x2, x3);
       }
     };
     if (active) {
       const bool full = (q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0);
-      if constexpr (ATTN_DKDV_STATIC) {
-        if (full) body(std::true_type{});
-        else body(std::false_type{});
-      } else {
-        body(full);
-      }
+      body(full);
     }
     if (more1) {  // n1's data (issued an iteration ago) landed; n2's DMAs may still be in flight
       if (more2) dma_wait<NV>();

@@ -27,10 +27,16 @@ enum { SITE_EMB = 0, SITE_ATTN = 1, SITE_MLP = 2 };
 struct Dims {
   int V, Vp, Tmax, L, H, KV, d, hd, kvd, Nqkv, hid, Hp, swiglu, rope;
   int G, dw_bm, dw_ks;  // blocks per grouped weight-gradient launch, its tile rows, token split
+  int force_ks;         // cfg.opts.dw_ksplit: 0 = the planner's choice
+  bool rem_first;       // cfg.opts.dw_remainder_first
+  long long plan_tokens;  // cfg.opts.dw_plan_tokens: plan as for this many tokens (0 = the step's)
 };
 
 bool dims_of(const cg_model_cfg* c, Dims& D) {
   if (!c || c->n_embd <= 0 || c->n_head <= 0 || c->n_embd % c->n_head) return false;
+  // engine options (zero = defaults): out-of-range values are an error, not a silent default
+  if (c->opts.dw_group < 0 || c->opts.dw_ksplit < 0 || c->opts.dw_ksplit > 3 || c->opts.dw_plan_tokens < 0)
+    return false;
   D.V = c->vocab_size;
   D.Vp = (int)rup(c->vocab_size, 16);
   D.Tmax = c->block_size;
@@ -48,6 +54,9 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   D.G = 1;
   D.dw_bm = 128;
   D.dw_ks = 1;
+  D.force_ks = c->opts.dw_ksplit;
+  D.rem_first = c->opts.dw_remainder_first != 0;
+  D.plan_tokens = c->opts.dw_plan_tokens;
   return true;
 }
 
@@ -59,17 +68,11 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
 // measured at K = 16384 on the C4/C5 shapes (tools/dw_grouped.py).  Each group takes its
 // cheapest tile (a short remainder group often prefers the smaller tile); the plan minimises the
 // summed cost of the groups (G, G, ..., remainder) and, on ties, prefers the smaller group (its
-// gradients are final -- and all-reduced -- earlier).  CG_DW_GROUP / CG_DW_BM force a choice.
+// gradients are final -- and all-reduced -- earlier).  cg_model_cfg.opts.dw_group / dw_ksplit force
+// a choice (tests, A/B runs).
 struct DwPlan {
   int G, bm, ks;  // group size, tile of a full group, its token-range split
 };
-static int dw_forced_bm() {
-  static const int forced = [] { const char* e = getenv("CG_DW_BM"); return e ? atoi(e) : 0; }();
-  return forced;
-}
-// 0: the planner's token-range split; 1..3: forced (CG_DW_KSPLIT / cg_set_dw_ksplit, for A/B and tests)
-static int g_dw_ks = [] { const char* e = getenv("CG_DW_KSPLIT"); return e ? atoi(e) : 0; }();
-static int dw_forced_ks() { return g_dw_ks; }
 // weight elements of one block's dW products (the slab a token-range split writes per slice)
 static long long dw_block_elems(const Dims& D) {
   const long long d = D.d;
@@ -80,12 +83,12 @@ static long long dw_block_elems(const Dims& D) {
 // tiles alone leave CUs idle: C2's 144 tiles on 256 CUs) plus a slab pass of ~20 B per weight
 // element and extra slice at ~5 TB/s, priced against ~11 ns per token for 1.0 of tile cost
 // (C2 / C3 rocprofv3: 495 us for a round of 1.38 at M = 32768)
-static int dw_tile_for(const Dims& D, int n, double* cost_out, int* ks_out = nullptr, long long M = 16384) {
+static int dw_tile_for(const Dims& D, int n, double* cost_out, int* ks_out, long long M) {
+  if (D.plan_tokens > 0) M = D.plan_tokens;
   const int d = D.d, cus = cg_pers_cus();
   int best = 256, best_ks = 1;
   double best_cost = 1e30;
   for (int bm : {128, 256, 512}) {
-    if (dw_forced_bm() && bm != dw_forced_bm()) continue;
     // (256 x 256: 2.35 at K = 16384 on C4/C5; 2.49 at C3, K = 32768: 951 vs 526 us per round of
     // the 256 x 128 tile, rocprofv3 -- 2.5 keeps C4 on its 5/5/2 plan and moves C3 from 6/4 to
     // 4/4/2, 9.08 -> 8.99 ms/step, profiles/round4/dw_sweep)
@@ -94,7 +97,7 @@ static int dw_tile_for(const Dims& D, int n, double* cost_out, int* ks_out = nul
                           (D.swiglu ? cg_gemm_dw_tiles(bm, 2 * D.Hp, d) + cg_gemm_dw_tiles(bm, d, D.Hp)
                                     : cg_gemm_dw_tiles(bm, D.hid, d) + cg_gemm_dw_tiles(bm, d, D.hid));
     for (int ks = 1; ks <= 3; ++ks) {
-      if (dw_forced_ks() && ks != dw_forced_ks()) continue;
+      if (D.force_ks && ks != D.force_ks) continue;
       const double slab = (double)(ks - 1) * n * dw_block_elems(D) * 20.0 / 5e12 / (11e-9 * (double)M);
       const double cost = (double)((n * per_layer * ks + cus - 1) / cus) * tile_cost / ks + slab;
       if (cost < best_cost - 1e-9) best_cost = cost, best = bm, best_ks = ks;
@@ -104,11 +107,9 @@ static int dw_tile_for(const Dims& D, int n, double* cost_out, int* ks_out = nul
   if (ks_out) *ks_out = best_ks;
   return best;
 }
-static int g_dw_group = [] { const char* e = getenv("CG_DW_GROUP"); return e ? atoi(e) : 0; }();
-static int g_dw_order = [] { const char* e = getenv("CG_DW_ORDER"); return e ? atoi(e) : 1; }();
-DwPlan dw_plan(const cg_model_cfg* c, const Dims& D, long long M = 16384) {
+DwPlan dw_plan(const cg_model_cfg* c, const Dims& D, long long M) {
   if (c->dtype != CG_BF16 || D.L <= 0) return {1, 128, 1};
-  const int forced_g = g_dw_group;
+  const int forced_g = c->opts.dw_group;
   const int gmax = std::min(D.L, CG_DW_MAX / 4);
   DwPlan best{1, 128, 1};
   double best_cost = 1e30;
@@ -216,17 +217,6 @@ struct WS {
   }
 };
 
-static int g_fused_keep = [] {
-  const char* e = getenv("CG_ATTN_FUSED_KEEP");
-  return e ? atoi(e) : 1;
-}();
-// RoPE models: the rotation fused into the qkv projection's epilogue (forward) and into the
-// attention backward's dQ / dK stores (backward) -- 1 (default; env CG_ROPE_FUSED at load) -- or
-// the separate cg_rope_tab passes (0; also the fallback where a kernel does not implement it)
-static int g_rope_epi = [] {
-  const char* e = getenv("CG_ROPE_FUSED");
-  return e ? atoi(e) : 1;
-}();
 struct LayerAct {
   float *mean1, *rstd1, *mean2, *rstd2, *lse, *xmid;
   void *h1, *qkv, *y, *h2, *a, *g, *gu, *s;
@@ -387,8 +377,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.embws = w.take<float>(A.nb.embws);
   A.nb.cews = cg_ce_workspace((int)M);
   A.cews = w.take<float>(A.nb.cews);
-  static const bool wt_env = [] { const char* e = getenv("CG_DX_TRANSPOSE"); return !e || atoi(e) != 0; }();
-  A.wT = wt_env && c->dtype == CG_BF16 && d % 8 == 0 && D.Nqkv % 8 == 0 && D.hid % 8 == 0 && D.Hp % 8 == 0;
+  A.wT = c->dtype == CG_BF16 && d % 8 == 0 && D.Nqkv % 8 == 0 && D.hid % 8 == 0 && D.Hp % 8 == 0;
   for (int l = 0; l < D.L; ++l) {
     auto& a = A.la[l];
     a.qkvT = a.pT = a.w1T = a.w2T = a.wguT = a.wdT = nullptr;
@@ -410,8 +399,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
     A.o1T[i] = w.take<char>((size_t)d * d * 2);
     A.o2T[i] = w.take<char>((size_t)d * d * 2);
   }
-  static const bool mask_env = [] { const char* e = getenv("CG_ATTN_DROP_MASK"); return !e || atoi(e) != 0; }();
-  const bool dmask = mask_env && c->dtype == CG_BF16 && c->dropout > 0.f;
+  const bool dmask = c->dtype == CG_BF16 && c->dropout > 0.f;
   for (int l = 0; l < D.L; ++l)
     A.la[l].dmask = dmask ? w.take<char>(cg_attn_drop_mask_bytes(B, T, D.H)) : nullptr;
   return w.off + 256;
@@ -594,7 +582,7 @@ float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 // are final after 2 blocks instead of 5.  tools/bucket_replay.py priced both on one GPU with the
 // all-reduces modelled as CU-holding side-stream kernels: 5/5/2 8.22 / 8.44 ms against 2/5/5
 // 8.31 / 8.63 ms per C4 step at 600 / 300 GB/s bus bandwidth.
-int first_group(const Dims& D) { return (g_dw_order == 0 && D.L % D.G) ? D.L % D.G : D.G; }
+int first_group(const Dims& D) { return (D.rem_first && D.L % D.G) ? D.L % D.G : D.G; }
 // position of block l inside its group, counted from the group's top block
 int slot_of(const Dims& D, int l) {
   const int u = D.L - 1 - l, f = first_group(D);
@@ -676,72 +664,6 @@ int head_dw_now(const Ctx& C, long long hoff, float alpha, int accumulate) {
 // (tok_emb) is final only after phase 2, so no data-parallel bucket sees it early.  The pending
 // product lives in the cg_model itself (head_dw_*), so its lifetime and thread ownership are the
 // model's; phase 0 (re)sets it, phase 2 runs it if no group did.
-static int g_head_dw_defer = [] {
-  const char* e = getenv("CG_HEAD_DW_DEFER");
-  return e ? atoi(e) : 1;
-}();
-}  // namespace
-extern "C" int cg_set_dw_order(int order) {
-  const int prev = g_dw_order;
-  g_dw_order = order ? 1 : 0;
-  return prev;
-}
-extern "C" int cg_set_dw_ksplit(int ks) {
-  const int prev = g_dw_ks;
-  g_dw_ks = ks < 0 || ks > 3 ? 0 : ks;
-  return prev;
-}
-
-extern "C" int cg_set_dw_group(int blocks) {
-  const int prev = g_dw_group;
-  g_dw_group = blocks < 0 ? 0 : blocks;
-  return prev;
-}
-extern "C" int cg_set_rope_fused(int on) {
-  const int old = g_rope_epi;
-  g_rope_epi = on != 0;
-  return old;
-}
-extern "C" int cg_set_head_dw_defer(int on) {
-  const int prev = g_head_dw_defer;
-  g_head_dw_defer = on ? 1 : 0;
-  return prev;
-}
-// 1 (env CG_DW_OVERLAP): the last dW group of a backward (blocks ending at block 0) runs on a side
-// stream while the main stream finishes block 0's LayerNorm backward, the deferred reductions and
-// the embedding backward -- meant to fill the CUs the group's tiles leave idle (C4: 192 tiles of
-// the 2-block group on 256 CUs); the main stream joins it before phase 1 returns, so the group's
-// bucket is final when the caller sees dw_done_layer == 0.  Default 0: measured slower on every
-// config (C4 7.652 -> 7.709 ms, C5 5.778 -> 5.952, C2 3.020 -> 3.068; the persistent dW walker
-// loses CUs to the streaming kernels while they run, profiles/round4/dw_overlap_ab.txt).
-static int g_dw_overlap = [] {
-  const char* e = getenv("CG_DW_OVERLAP");
-  return e ? atoi(e) : 0;
-}();
-extern "C" int cg_set_dw_overlap(int on) {
-  const int prev = g_dw_overlap;
-  g_dw_overlap = on ? 1 : 0;
-  return prev;
-}
-namespace {
-// per-device side stream and fork / join events (created once, never destroyed)
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-SideStream* side_stream() {
-  static SideStream ss[64];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& x = ss[dev];
-  if (!x.s) {
-    if (hipStreamCreateWithFlags(&x.s, hipStreamNonBlocking) != hipSuccess) return x.s = nullptr, nullptr;
-    if (hipEventCreateWithFlags(&x.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&x.join, hipEventDisableTiming) != hipSuccess)
-      return nullptr;
-  }
-  return &x;
-}
 }  // namespace
 
 namespace {
@@ -948,12 +870,13 @@ extern "C" int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* ou
   return n;
 }
 
-extern "C" int cg_model_dw_plan(const cg_model_cfg* cfg, int* group_layers, int* tile_m) {
+extern "C" int cg_model_dw_plan(const cg_model_cfg* cfg, int B, int T, int* group_layers, int* tile_m, int* ksplit) {
   Dims D;
-  if (!dims_of(cfg, D)) return CG_EINVAL;
-  const DwPlan pl = dw_plan(cfg, D);
+  if (!dims_of(cfg, D) || B <= 0 || T <= 0) return CG_EINVAL;
+  const DwPlan pl = dw_plan(cfg, D, (long long)B * T);
   if (group_layers) *group_layers = pl.G;
   if (tile_m) *tile_m = pl.bm;
+  if (ksplit) *ksplit = pl.ks;
   return CG_OK;
 }
 
@@ -966,39 +889,6 @@ extern "C" size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T
   D.dw_ks = pl.ks;
   Acts A;
   return carve(cfg, D, B, T, nullptr, A);
-}
-
-// The attention keep-bit arrays depend only on (seed, layer, B, T, H): all layers' arrays are
-// generated on a side stream at the start of the forward, concurrently with the embedding, the
-// LayerNorms and the GEMMs of the first layers (pure-VALU work beside MFMA / DMA-bound kernels);
-// layer l's attention waits on its event.  The side stream first waits for everything already
-// on the caller's stream (the previous backward still reads the arrays).  Off by default
-// (CG_ATTN_MASK_SIDE=1 enables it): measured at C4 it made the step 0.07 ms SLOWER (8.875 vs
-// 8.80 ms, same box) -- the generator's small workgroups delay the dispatch of the main stream's
-// persistent GEMMs more than their VALU work hides beside them.  Default: in order, just before
-// each layer's attention.
-struct MaskStream {
-  hipStream_t s = nullptr;
-  hipEvent_t start = nullptr;
-  std::vector<hipEvent_t> done;
-};
-static MaskStream* mask_stream(int layers) {
-  static const bool on = [] { const char* e = getenv("CG_ATTN_MASK_SIDE"); return e && atoi(e) != 0; }();
-  static MaskStream per_dev[16];
-  if (!on) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return nullptr;
-  MaskStream& ms = per_dev[dev];
-  if (!ms.s) {
-    if (hipStreamCreateWithFlags(&ms.s, hipStreamNonBlocking) != hipSuccess) return ms.s = nullptr, nullptr;
-    if (hipEventCreateWithFlags(&ms.start, hipEventDisableTiming) != hipSuccess) return nullptr;
-  }
-  while ((int)ms.done.size() < layers) {
-    hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    ms.done.push_back(e);
-  }
-  return &ms;
 }
 
 extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* targets, int B, int T, int training,
@@ -1022,18 +912,11 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   const float eps = m->cfg.ln_eps > 0 ? m->cfg.ln_eps : 1e-5f;
   m->logits = logits ? logits : A.logits_int;
 
-  // the keep bits: made by each block's attention forward itself (default), or by the mask kernel
-  // on a side stream ahead of the forward (CG_ATTN_FUSED_KEEP=0)
-  const bool masks = p > 0.f && D.L > 0 && A.la[0].dmask && !g_fused_keep;
-  MaskStream* ms = masks ? mask_stream(D.L) : nullptr;
-  if (ms) {
-    if (hipEventRecord(ms->start, C.s) != hipSuccess || hipStreamWaitEvent(ms->s, ms->start, 0) != hipSuccess)
-      return CG_ELAUNCH;
-    for (int l = 0; l < D.L; ++l) {
-      CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, A.la[l].dmask, ms->s));
-      if (hipEventRecord(ms->done[l], ms->s) != hipSuccess) return CG_ELAUNCH;
-    }
-  }
+  // the attention keep bits: written by each block's attention forward itself (default), or by the
+  // mask kernel right before it (cfg.opts.attn_mask_kernel; a mask pass on a side stream ahead of
+  // the forward measured slower, round 2)
+  const bool fused_keep = !m->cfg.opts.attn_mask_kernel;
+  const bool rope_epi = !m->cfg.opts.rope_tables;
   CK(cg_segment_starts(idx, A.seg, B, T, m->cfg.sep_id, C.s));
   CK(cg_embed_fwd(idx, P(C, C.Lo.tok), C.Lo.pos >= 0 ? P(C, C.Lo.pos) : nullptr, A.x, B, T, d,
                   site_seed(seed, -1, SITE_EMB), p, C.s));
@@ -1047,7 +930,7 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     g.epilogue = CG_EPI_BIAS; g.bias = P(C, o.bqkv);
     // RoPE in the projection's epilogue where the GEMM tile implements it, else a table pass
     int rc_rope = CG_EUNSUPPORTED;
-    if (D.rope && g_rope_epi) {
+    if (D.rope && rope_epi) {
       cg_gemm_desc gr = g;
       gr.epilogue |= CG_EPI_ROPE;
       gr.rope_cos = m->rope_cos; gr.rope_sin = m->rope_sin;
@@ -1060,15 +943,11 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
       if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
     }
     const void* dmask = p > 0.f ? a.dmask : nullptr;
-    if (dmask && g_fused_keep) {
+    if (dmask && fused_keep) {
       CK(cg_attn_fwd_keep(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV,
                           D.hd, window, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
     } else {
-      if (dmask && ms) {
-        if (hipStreamWaitEvent(C.s, ms->done[l], 0) != hipSuccess) return CG_ELAUNCH;
-      } else if (dmask) {
-        CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
-      }
+      if (dmask) CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
       CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
                      window, site_seed(seed, l, SITE_ATTN), p, dmask, C.s));
     }
@@ -1193,7 +1072,6 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
 
   if (phase == 0) {
     pending(m).n = 0;  // a backward starts here: drop anything an abandoned one left
-    m->embed_done = 0;
     CK(transpose_weights(C));  // this step's shadow weights -> K-contiguous dX operands
     const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
     CK(fill_head2(C, hoff));
@@ -1204,7 +1082,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     if (m->targets) {
       // d(head weight) = s dlogits^T . xf: deferred into the first dW group when nothing else
       // adds into it before that launch (the aux heads do, and reuse dlogits)
-      if (g_head_dw_defer && C.dt == CG_BF16 && D.L > 0 && m->cfg.tie_embeddings && !m->cfg.termination_aux &&
+      if (!m->cfg.opts.head_dw_separate && C.dt == CG_BF16 && D.L > 0 && m->cfg.tie_embeddings && !m->cfg.termination_aux &&
           m->cfg.n_offsets <= 0)
       {
         m->head_dw_off = hoff;
@@ -1282,7 +1160,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // the partials), else a colsum pass after the vector kernels and the table inverse rotation
     const void* segp = m->cfg.sep_id >= 0 ? A.seg : nullptr;
     const void* dmask_b = p > 0.f ? a.dmask : nullptr;
-    const bool rope_in = D.rope && g_rope_epi;  // the inverse rotation inside the kernels
+    const bool rope_in = D.rope && !m->cfg.opts.rope_tables;  // the inverse rotation inside the kernels
     const float* rc_cos = rope_in ? m->rope_cos : nullptr;
     const float* rc_sin = rope_in ? m->rope_sin : nullptr;
     int rc = CG_EUNSUPPORTED;
@@ -1305,20 +1183,10 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       CK(bias_grad(C, sl.dqkv, D.Nqkv, D.Nqkv, o.bqkv, accumulate));
     g = lin_dx(C, sl.dqkv, D.Nqkv, o.wqkv, d, D.Nqkv, d, A.dsmall, d, a.qkvT);  // dL/d(ln1 out)
     CK(cg_gemm(&g, C.s));
-    // the group's weight gradients once its lowest block is done; the last group (l == 0) on the
-    // side stream, joined below (see g_dw_overlap)
-    SideStream* ss = (l == 0 && group_ends(D, l) && g_dw_overlap) ? side_stream() : nullptr;
-    // the tied head's deferred product in this group writes tok_emb's gradient: the embedding
-    // backward then stays behind the join
-    const bool embed_early = ss && !m->head_dw_pending;
-    if (ss) {
-      if (hipEventRecord(ss->fork, C.s) != hipSuccess || hipStreamWaitEvent(ss->s, ss->fork, 0) != hipSuccess)
-        return CG_ELAUNCH;
-      Ctx C2 = C;
-      C2.s = ss->s;
-      CK(flush_dw(C2, l + slot_of(D, l), l, accumulate));
-      if (hipEventRecord(ss->join, ss->s) != hipSuccess) return CG_ELAUNCH;
-    } else if (group_ends(D, l)) {
+    // the group's weight gradients once its lowest block is done.  (The last group on a side
+    // stream beside block 0's LayerNorm backward and the embedding backward measured slower on
+    // every config, round 4: the persistent walker loses CUs to the streaming kernels.)
+    if (group_ends(D, l)) {
       CK(flush_dw(C, l + slot_of(D, l), l, accumulate));
       m->dw_done_layer = l;
     }
@@ -1331,14 +1199,6 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // the group's parameter-gradient reductions (its LayerNorms, fused biases) in one launch,
     // before the caller starts the group's bucket all-reduce
     if (group_ends(D, l)) CK(flush_reduce(m, C.s));
-    if (ss) {
-      if (embed_early) {
-        CK(embed_backward(C, m, seed, p, accumulate));
-        m->embed_done = 1;
-      }
-      if (hipStreamWaitEvent(C.s, ss->join, 0) != hipSuccess) return CG_ELAUNCH;
-      m->dw_done_layer = l;
-    }
     return CG_OK;
   }
   if (phase == 2) {
@@ -1347,8 +1207,7 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
       m->head_dw_pending = 0;
       CK(head_dw_now(C, m->head_dw_off, m->head_dw_alpha, m->head_dw_accumulate));
     }
-    if (!m->embed_done) CK(embed_backward(C, m, seed, p, accumulate));
-    m->embed_done = 0;
+    CK(embed_backward(C, m, seed, p, accumulate));
     return CG_OK;
   }
   return CG_EINVAL;
@@ -1543,9 +1402,9 @@ extern "C" size_t cg_struct_bytes(const char* name) {
   if (n == #T) return sizeof(T);
   CG_SZ(cg_gemm_desc) CG_SZ(cg_dw_product) CG_SZ(cg_dw_group) CG_SZ(cg_reduce_job) CG_SZ(cg_reduce_batch)
   CG_SZ(cg_transpose_item) CG_SZ(cg_transpose_batch) CG_SZ(cg_adamw_segment) CG_SZ(cg_model_cfg)
-  CG_SZ(cg_param_entry) CG_SZ(cg_model)
+  CG_SZ(cg_param_entry) CG_SZ(cg_model) CG_SZ(cg_model_opts)
 #undef CG_SZ
   return 0;
 }
 
-extern "C" const char* cg_version(void) { return "codonlm_hip 0.3 gfx950"; }
+extern "C" const char* cg_version(void) { return "codonlm_hip 0.4 gfx950"; }

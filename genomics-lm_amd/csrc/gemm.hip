@@ -591,8 +591,6 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_vec_kernel(GemmParams p) {
 #include "gemm_wide.h"
 #include "gemm_pers.h"
 #include "gemm_lw.h"
-#include "gemm_pp.h"
-#include "gemm_pp2.h"
 #include "gemm_dw.h"
 
 // CG_EPI_COLSUM fallback: part[r/64][n] = sum of C rows [64r, 64r+64) (column n)
@@ -649,98 +647,38 @@ struct VecK { static constexpr gemm_kernel_t fn = gemm_bf16_vec_kernel<AK, BKC, 
 template <bool AK, bool BKC, int E, int T>
 struct WideK { static constexpr gemm_kernel_t fn = gemm_bf16_wide_kernel<AK, BKC, E, T>; };
 
-// persistent 256x128 tile (K-contiguous operands only, compile-time epilogues only)
-// loader-wave variant (gemm_lw.h).  Measured per C4 product (tools/gemm_c4.py, CG_PERS_LW=0/1
-// interleaved on one box) it takes qkv dX 28.3 -> 26.9 us and fc1 dX 35.0 -> 32.7 us (qkv fwd
-// and proj dX unchanged), while the VALU- and memory-heavy epilogues (GELU, dGELU + column sums,
-// fp32 residual) run 1.2-2.3 us slower in it; with it on the plain / bias-only products the
-// whole C4 step measured 8.45 vs 8.41 ms on one box (bench.py, 2 x 2 interleaved runs) but
-// 7.971 vs 8.034 and 8.05 vs 8.12 ms on two later boxes (3 x 2 and 2 x 3 interleaved runs, round 3):
-// mode 1 is the default.  Mode (env CG_PERS_LW at load, or cg_gemm_set_pers_lw): 0 never, 1 for the
-// epilogues listed in pers_lw_for (round 4: widened from plain / bias-only), 2 for every epilogue it
-// implements.
-// fp32 products on the 128x128 f32-MFMA tile: 2 (default; env CG_F32_BIG) every operand layout,
-// 1 only K-contiguous x K-contiguous (the forward), 0 never (the 64x64 kernel: A/B switch)
-static int g_f32_big = [] {
-  const char* e = getenv("CG_F32_BIG");
-  return e ? atoi(e) : 2;
-}();
-static int g_pers_lw = [] {
-  const char* e = getenv("CG_PERS_LW");
-  return e ? atoi(e) : 1;
-}();
-extern "C" int cg_gemm_set_pers_lw(int mode) {
-  const int old = g_pers_lw;
-  g_pers_lw = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
-  return old;
+// Tile choice per call (cg_gemm_desc.tile; the library keeps no mutable process-wide settings).
+// CG_TILE_AUTO: the persistent 256x128 tile whenever it is legal (K-contiguous operands, no split,
+// an epilogue it implements), on its loader-wave variant (gemm_lw.h) for the epilogues measured
+// faster there (round 3-4, tools/gemm_c4.py same box: qkv dX 28.3 -> 26.9 us, fc1 dX 35.0 -> 32.7,
+// fc1 forward GELU' 54.7 -> 52.0, proj forward bias + fp32 residual 23.5 -> 22.0, C3 SwiGLU forward
+// 90.2 -> 87.4; the dGELU, dropout-residual and column-sum epilogues stay on the 8-wave kernel:
+// fc2 dX 52.1 vs 53.5, fc2 forward 49.8 vs 51.5 on the loader-wave one); else the 256x128 LDS-DMA
+// tile for K-contiguous products with >= 192 tiles; else the 128x128 register-staged tile.
+// The other codes force one kernel for tests and A/B runs (CG_EUNSUPPORTED where it cannot run
+// the product).  fp32 products always take the 128x128 f32-MFMA tile where its 16-B operand
+// chunks are legal, else the 64x64 one.
+static bool lw_auto_for(int e) {
+  return e == 0 || e == CG_EPI_BIAS || e == (CG_EPI_BIAS | CG_EPI_GELU) ||
+         e == (CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV) || e == (CG_EPI_BIAS | CG_EPI_RESID) ||
+         e == CG_EPI_RESID || e == CG_EPI_SWIGLU || (e & CG_EPI_ROPE);
 }
-// the ping-pong kernel (gemm_pp.h): 0 off, 1 (env CG_PERS_PP at load) for products without an
-// epilogue or with a bias only, 2 for every epilogue
-static int g_pers_pp = [] {
-  const char* e = getenv("CG_PERS_PP");
-  return e ? atoi(e) : 0;
-}();
-extern "C" int cg_gemm_set_pers_pp(int mode) {
-  const int old = g_pers_pp;
-  g_pers_pp = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
-  return old;
-}
-static bool pers_pp_for(int e) {
-  if (e & CG_EPI_ROPE) return false;
-  if (g_pers_pp == 2) return true;
-  return g_pers_pp == 1 && (e == 0 || e == CG_EPI_BIAS);
-}
-// the SwiGLU backward's epilogue does not fit the loader-wave kernel's 168-register budget
-static bool pers_lw_for(int e) {
-  if (pers_pp_for(e)) return false;
-  if (e & CG_EPI_ROPE) return g_pers_lw != 0;  // the RoPE epilogue is the loader-wave kernel's only
-  if (g_pers_lw == 2) return e != CG_EPI_DSWIGLU;
-  // mode 1: the epilogues measured faster on it (round 4, rocprofv3 per kernel, same box: C4 fc1
-  // forward GELU' 54.7 -> 52.0 us, proj forward bias + fp32 residual 23.5 -> 22.0, C3 SwiGLU forward
-  // 90.2 -> 87.4); the dGELU / dropout-residual / column-sum ones stay on the 8-wave kernel
-  // (C4 fc2 dX 52.1 -> 53.5, fc2 forward 49.8 -> 51.5 on it)
-  return g_pers_lw == 1 && (e == 0 || e == CG_EPI_BIAS || e == (CG_EPI_BIAS | CG_EPI_GELU) ||
-                            e == (CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV) ||
-                            e == (CG_EPI_BIAS | CG_EPI_RESID) || e == CG_EPI_RESID || e == CG_EPI_SWIGLU);
-}
-// the 256x256 ping-pong kernel (gemm_pp2.h) for bf16-output products with at least one 256-wide
-// column tile per CU-round: 0 off, 1 (env CG_PERS_PP2 at load)
-static int g_pers_pp2 = [] {
-  const char* e = getenv("CG_PERS_PP2");
-  return e ? atoi(e) : 0;
-}();
-extern "C" int cg_gemm_set_pers_pp2(int mode) {
-  const int old = g_pers_pp2;
-  g_pers_pp2 = mode < 0 ? 0 : (mode > 1 ? 1 : mode);
-  return old;
-}
-static gemm_kernel_t pick_pp2(int e, int ct) {
-  if (ct != CG_BF16) return nullptr;
-#define P2SPEC(E) \
-  if (e == (E)) return gemm_bf16_pp2_kernel<(E)>;
-  P2SPEC(0)
-  P2SPEC(CG_EPI_BIAS)
-  P2SPEC(CG_EPI_BIAS | CG_EPI_GELU)
-  P2SPEC(CG_EPI_BIAS | CG_EPI_GELU | CG_EPI_GELU_DERIV)
-  P2SPEC(CG_EPI_DGELU)
-  P2SPEC(CG_EPI_DGELU | CG_EPI_GELU_DERIV)
-  P2SPEC(CG_EPI_DGELU | CG_EPI_COLSUM)
-  P2SPEC(CG_EPI_DGELU | CG_EPI_GELU_DERIV | CG_EPI_COLSUM)
-  P2SPEC(CG_EPI_COLSUM)
-#undef P2SPEC
-  return nullptr;
-}
-static gemm_kernel_t pick_pers(int e, int ct) {
+// the persistent kernel for epilogue e, output type ct under tile code `tile` (nullptr: none)
+static gemm_kernel_t pick_pers(int e, int ct, int tile, bool* lw_out) {
+  bool lw = tile == CG_TILE_PERS_LW || (tile == CG_TILE_AUTO && lw_auto_for(e));
+  // the SwiGLU backward's epilogue does not fit the loader-wave kernel's 168-register budget;
+  // the RoPE epilogue exists only there
+  if (e == CG_EPI_DSWIGLU) lw = false;
   if (e & CG_EPI_ROPE) {
-    if (ct != CG_BF16 || !pers_lw_for(e)) return nullptr;
+    if (ct != CG_BF16 || !lw) return nullptr;
+    *lw_out = true;
     if (e == (CG_EPI_BIAS | CG_EPI_ROPE)) return gemm_bf16_lw_kernel<CG_EPI_BIAS | CG_EPI_ROPE, CG_BF16>;
     if (e == CG_EPI_ROPE) return gemm_bf16_lw_kernel<CG_EPI_ROPE, CG_BF16>;
     return nullptr;
   }
-#define PSPEC(E, T)                                                                              \
-  if (e == (E) && ct == (T))                                                                    \
-    return pers_pp_for(e) ? gemm_bf16_pp_kernel<(E), (T)>                                       \
-                          : pers_lw_for(e) ? gemm_bf16_lw_kernel<(E), (T)> : gemm_bf16_pers_kernel<(E), (T)>;
+  *lw_out = lw;
+#define PSPEC(E, T) \
+  if (e == (E) && ct == (T)) return lw ? gemm_bf16_lw_kernel<(E), (T)> : gemm_bf16_pers_kernel<(E), (T)>;
   PSPEC(0, CG_BF16)
   PSPEC(0, CG_F32)
   PSPEC(CG_EPI_BIAS, CG_BF16)
@@ -761,45 +699,29 @@ static gemm_kernel_t pick_pers(int e, int ct) {
 #undef PSPEC
   return nullptr;
 }
-static int g_pers_mode = [] {
-  const char* e = getenv("CG_GEMM_PERS");
-  return e ? atoi(e) : 1;  // 1 = persistent tile whenever legal (grid = CUs), 0 = never, N>1: grid capped at N
-}();
-extern "C" int cg_gemm_set_pers(int mode) {
-  const int old = g_pers_mode;
-  g_pers_mode = mode < 0 ? 0 : mode;
-  return old;
-}
 static int cu_count() {
   static int n[64] = {0};
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (dev < 0 || dev >= 64) dev = 0;
-  if (!n[dev]) {
+  if (!n[dev]) {  // a benign race: every thread stores the same value
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
     n[dev] = v;
   }
   return n[dev];
 }
-// CUs the persistent launches (forward / dX tiles, grouped dW) spread over: all of them, minus a
-// reserve left free for kernels that run beside them (the RCCL all-reduce of a data-parallel
-// backward, which otherwise holds CUs a one-tile-per-CU launch is waiting for)
-static int g_cu_reserve = [] {
-  const char* e = getenv("CG_PERS_CU_RESERVE");
-  return e ? std::max(0, atoi(e)) : 0;
-}();
-extern "C" int cg_set_cu_reserve(int n) {
-  const int old = g_cu_reserve;
-  g_cu_reserve = n < 0 ? 0 : n;
-  return old;
-}
-extern "C" int cg_pers_cus(void) { return std::max(1, cu_count() - g_cu_reserve); }
+// CUs the persistent launches (forward / dX tiles, grouped dW) spread over.  (A reserve of CUs
+// left free for an RCCL all-reduce beside the backward was measured and removed in round 5: a
+// one-tile-per-CU launch becomes two rounds either way)
+extern "C" int cg_pers_cus(void) { return cu_count(); }
 static bool use_pers(const cg_gemm_desc* d, int split) {
-  if (!g_pers_mode || split != 1) return false;
+  if (split != 1) return false;
+  if (d->tile != CG_TILE_AUTO && d->tile != CG_TILE_PERS && d->tile != CG_TILE_PERS_LW) return false;
   if (!d->a_kcontig || !d->b_kcontig) return false;
   if (d->K % bfp::BKT || d->K < 2 * bfp::BKT) return false;
-  if (!pick_pers(d->epilogue, d->c_dtype)) return false;
+  bool lw = false;
+  if (!pick_pers(d->epilogue, d->c_dtype, d->tile, &lw)) return false;
   // every buffer extent must stay below the out-of-range voffset used for masked lanes
   const long long lim = (long long)bfp::OOR - (1ll << 24);
   const long long es = d->c_dtype == CG_BF16 ? 2 : 4;
@@ -819,21 +741,10 @@ static bool use_pers(const cg_gemm_desc* d, int split) {
 }
 
 // 256x128 LDS-DMA tile: large, 64-aligned K chunks and enough tiles to fill the chip
-static int g_wide_mode = [] {
-  const char* e = getenv("CG_GEMM_WIDE");
-  return e ? atoi(e) : -1;  // -1 auto, 0 never, 1 whenever legal
-}();
-static int wide_mode() { return g_wide_mode; }
-extern "C" int cg_gemm_set_wide(int mode) {
-  const int old = g_wide_mode;
-  g_wide_mode = mode < 0 ? -1 : (mode > 0 ? 1 : 0);
-  return old;
-}
 static bool use_wide(const cg_gemm_desc* d, int kchunk, int split) {
-  const int mode = wide_mode();
-  if (mode == 0) return false;
+  if (d->tile != CG_TILE_AUTO && d->tile != CG_TILE_WIDE) return false;
   if (d->K % bfw::BKT || kchunk % bfw::BKT || d->M < bfw::BM || d->N < bfw::BN) return false;
-  if (mode == 1) return true;
+  if (d->tile == CG_TILE_WIDE) return true;
   // auto: the LDS-DMA tile wins on K-contiguous operands (forward products); with an
   // MN-contiguous operand (dX, dW) the 128x128 register-staged tile is still faster
   if (!d->a_kcontig || !d->b_kcontig) return false;
@@ -921,10 +832,9 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     p.epi &= ~CG_EPI_COLSUM;
     // the 128x128 f32-MFMA tile: 16-B operand chunks (leading dims and the contiguous extent of
     // each operand -- K for a K-contiguous one, M / N for an MN-contiguous one -- multiples of 4)
-    const bool big = g_f32_big && !(d->lda & 3) && !(d->ldb & 3) && !((uintptr_t)d->A & 15) &&
+    const bool big = !(d->lda & 3) && !(d->ldb & 3) && !((uintptr_t)d->A & 15) &&
                      !((uintptr_t)d->B & 15) && ((d->a_kcontig || d->b_kcontig) ? !(d->K & 3) : true) &&
-                     (d->a_kcontig || !(d->M & 3)) && (d->b_kcontig || !(d->N & 3)) &&
-                     (g_f32_big > 1 || (d->a_kcontig && d->b_kcontig));
+                     (d->a_kcontig || !(d->M & 3)) && (d->b_kcontig || !(d->N & 3));
     if (big) {
       launch4(gemm_f32_big_kernel<false, false>, gemm_f32_big_kernel<false, true>, gemm_f32_big_kernel<true, false>,
               gemm_f32_big_kernel<true, true>, d->a_kcontig, d->b_kcontig,
@@ -948,31 +858,23 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     if ((swg || rope) && !pers) return CG_EUNSUPPORTED;
     if (!pers) p.epi &= ~CG_EPI_COLSUM;  // only the persistent tile fuses the column sums
     const int ke = split > 1 ? 0 : p.epi, kt = split > 1 ? CG_F32 : p.c_dtype;
-    // 256x256 tiles: the products with N >= 1024 (at M = B.T >= 4096 at least one round of
-    // 256-wide tiles over the CUs) -- see gemm_pp2.h
-    const bool pp2 = pers && g_pers_pp2 && pick_pp2(p.epi, p.c_dtype) && p.N >= 1024 && p.K % bp2::BK == 0 &&
-                     (long long)cg_cdiv(p.M, bp2::BM) * cg_cdiv(p.N, bp2::BN) >= cg_pers_cus();
-    if (pp2) {
-      k = pick_pp2(p.epi, p.c_dtype);
-      colsum_fused = colsum;
-      const int tiles = cg_cdiv(p.N, bp2::BN) * cg_cdiv(p.M, bp2::BM);
-      g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cg_pers_cus()));
-      blk = dim3(bp2::THREADS);
-      sh = bp2::SMEM;
-    } else if (pers) {
-      k = pick_pers(p.epi, p.c_dtype);
+    if (pers) {
+      bool lw = false;
+      k = pick_pers(p.epi, p.c_dtype, d->tile, &lw);
       colsum_fused = colsum;
       const int tiles = cg_cdiv(p.N, (p.epi & CG_EPI_SWIGLU) ? bfp::BN / 2 : bfp::BN) * cg_cdiv(p.M, bfp::BM);
-      g = dim3(std::min(tiles, g_pers_mode > 1 ? g_pers_mode : cg_pers_cus()));
-      blk = dim3(pers_pp_for(p.epi) ? bpp::THREADS : pers_lw_for(p.epi) ? bfl::THREADS : bfp::THREADS);
-      sh = pers_pp_for(p.epi) ? bpp::SMEM : pers_lw_for(p.epi) ? bfl::SMEM : bfp::SMEM;
+      g = dim3(std::min(tiles, d->max_wg > 0 ? d->max_wg : cg_pers_cus()));
+      blk = dim3(lw ? bfl::THREADS : bfp::THREADS);
+      sh = lw ? bfl::SMEM : bfp::SMEM;
     } else if (vec && use_wide(d, kchunk, split)) {
       k = pick_spec<WideK>(d->a_kcontig, d->b_kcontig, ke, kt);
       g = dim3(cg_cdiv(p.N, bfw::BN) * cg_cdiv(p.M, bfw::BM) * split);
       blk = dim3(bfw::THREADS);
       sh = bfw::SMEM;
-    } else if (vec) {
+    } else if (vec && (d->tile == CG_TILE_AUTO || d->tile == CG_TILE_VEC)) {
       k = pick_spec<VecK>(d->a_kcontig, d->b_kcontig, ke, kt);
+    } else if (d->tile != CG_TILE_AUTO && d->tile != CG_TILE_VEC) {
+      return CG_EUNSUPPORTED;  // the forced tile cannot run this product
     } else {
       k = d->a_kcontig ? (d->b_kcontig ? gemm_bf16_kernel<true, true> : gemm_bf16_kernel<true, false>)
                        : (d->b_kcontig ? gemm_bf16_kernel<false, true> : gemm_bf16_kernel<false, false>);
@@ -1029,20 +931,11 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
 // ---------------------------------------------------------------------------
 // grouped weight-gradient GEMM (gemm_dw.h)
 // ---------------------------------------------------------------------------
-static int g_dw_bm = [] {
-  const char* e = getenv("CG_DW_BM");
-  return e ? atoi(e) : 128;
-}();
 static bool dw_tile_code(int bm) { return bm == 128 || bm == 129 || bm == 256 || bm == 512; }
-extern "C" int cg_gemm_dw_set_tile(int bm) {
-  const int old = g_dw_bm;
-  if (dw_tile_code(bm)) g_dw_bm = bm;
-  return old;
-}
 // tile codes: 128 / 129 = 128 x 128 (4 / 5 ring stages), 256 = 256 x 128 (3 stages),
 // 512 = 256 x 256 (2 stages of 64 KiB)
 extern "C" int cg_gemm_dw_tiles(int bm, int N_out, int K_out) {
-  if (!dw_tile_code(bm)) bm = g_dw_bm;
+  if (!dw_tile_code(bm)) bm = 128;
   return cg_cdiv(N_out, bm >= 256 ? 256 : 128) * cg_cdiv(K_out, bm == 512 ? 256 : 128);
 }
 template <int BM, int NS, int BNT = bfd::BN>
@@ -1058,7 +951,7 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   P.ntiles = ntiles * P.ksplit;
   if (!ntiles) return CG_OK;
   if (P.ksplit > 1) P.kc_steps = cg_cdiv(cg_cdiv(P.K, P.ksplit), bfd::BKT);
-  const int grid = std::min(P.ntiles, cg_pers_cus());
+  const int grid = std::min(P.ntiles, P.max_wg > 0 ? P.max_wg : cg_pers_cus());
   (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             G::SMEM);
   double flops = 0, bytes = 0;
@@ -1126,7 +1019,8 @@ extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
     P.slab_stride = off;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int bm = grp->tile_m > 0 ? grp->tile_m : g_dw_bm;
+  const int bm = grp->tile_m > 0 ? grp->tile_m : 128;
+  P.max_wg = grp->max_wg;
   // tile_m codes: 128 / 256 = rows of the C tile (ring of 4 / 3 stages); 129 / 257 = the same
   // tile with one more ring stage (5 / 4... 160 KB LDS for 128)
   if (bm == 512) return launch_dw<256, 2, 256>(P, s);

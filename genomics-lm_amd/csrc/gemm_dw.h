@@ -75,6 +75,7 @@ struct Params {
   // ([N_out][K_out] at slab + (s-1) slab_stride + the product's slab_off), added into C by
   // dw_slab_reduce_kernel in slice order
   int ksplit, kc_steps;
+  int max_wg;  // grid cap (0: one workgroup per CU)
   float* slab;
   long long slab_stride;
   long long slab_off[CG_DW_MAX];

@@ -21,31 +21,15 @@
 // source) are loaded two k-steps before the tile's end (or partly after its MFMAs where the
 // registers do not allow it) and waited for with vmcnt(0) -- no counted interleaving with the
 // DMA stream.
-// timing-only diagnostic builds of the RoPE epilogue (results invalid), bit set: 1 no table loads,
-// 2 B rows in natural order, 4 no rotation arithmetic, 8 C stores at the natural column positions
-#ifndef CG_ROPE_DIAG
-#define CG_ROPE_DIAG 0
-#endif
-// A-operand L2 prefetch (experiment): the loaders also issue, per stage, 4-byte LDS-DMA reads of the
-// A rows CG_LW_PF stages ahead of the stage they stream (into a scratch slot nobody reads), so the
-// HBM misses of a tile's A rows are taken that far ahead; 0 = off
-#ifndef CG_LW_PF
-#define CG_LW_PF 0
-#endif
-// residual L2 prefetch (experiment): with the fp32-residual epilogue each loader also issues, per
-// stage, one 4-byte LDS-DMA read per lane (into a scratch slot nobody reads) touching one 128-B line
-// of the tile's residual block, so the first 4 k-steps of a tile pull its 1024 residual lines
-// toward the CU while the MFMAs run instead of in the epilogue's burst; 0 = off
-#ifndef CG_LW_RPF
-#define CG_LW_RPF 0
-#endif
+// (Measured and removed, round 4: an L2 prefetch of the A rows a few stages ahead by the loaders,
+// 10-18 % slower; an L2 prefetch of the fp32-residual block during a tile's first k-steps, slower --
+// DESIGN.md section 10.)
 namespace bfl {
 constexpr int CWAVES = 8, LWAVES = 4, THREADS = 64 * (CWAVES + LWAVES);
 constexpr int A_PIECES = bfw::A_BYTES / 1024, B_PIECES = bfw::B_BYTES / 1024;  // 32, 16 per stage
 constexpr int LA = A_PIECES / LWAVES, LB = B_PIECES / LWAVES;                  // 8, 4 per loader
 constexpr int PER_STAGE = LA + LB;                                             // DMAs per loader per stage
-constexpr int PF_OPS = CG_LW_PF ? LA : 0;                                      // prefetch reads per stage
-constexpr int SMEM = bfp::SMEM + (CG_LW_PF || CG_LW_RPF ? LWAVES * 256 : 0);
+constexpr int SMEM = bfp::SMEM;
 }  // namespace bfl
 
 template <int EPI, int CT>
@@ -88,9 +72,6 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
     const int L = wave - bfl::CWAVES;
     const __amdgpu_buffer_rsrc_t ra = rsrc(p.A, ((long long)(p.M - 1) * p.lda + p.K) * 2);
     const __amdgpu_buffer_rsrc_t rb = rsrc(p.B, ((long long)((SWG ? 2 : 1) * p.N - 1) * p.ldb + p.K) * 2);
-    const __amdgpu_buffer_rsrc_t rres =
-        rsrc((EPI & CG_EPI_RESID) ? (const void*)p.resid : (const void*)p.A,
-             (EPI & CG_EPI_RESID) ? ((long long)(p.M - 1) * p.ldr + p.N) * 4 : 0);
     uint32_t va[bfl::LA], vb[bfl::LB];
 #pragma unroll
     for (int j = 0; j < bfl::LA; ++j) va[j] = bfw::src_off<true>((L + bfl::LWAVES * j) * 1024 + 16 * lane, p.lda);
@@ -111,7 +92,7 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
       for (int j = 0; j < bfl::LB; ++j) {
         const int pos = (L + bfl::LWAVES * j) * 1024 + 16 * lane;
         const int row = pos >> 7, phys = (pos >> 4) & 7;
-        vnext[j] = ((uint32_t)((CG_ROPE_DIAG & 2) ? n0 + row : rope_col(n0 + row)) * (uint32_t)p.ldb + 8u * (uint32_t)(phys ^ fb(row))) * 2u;
+        vnext[j] = ((uint32_t)rope_col(n0 + row) * (uint32_t)p.ldb + 8u * (uint32_t)(phys ^ fb(row))) * 2u;
       }
     };
     // stage g: the DMA origins of its (tile, k-step); past the CU's last stage every piece reads
@@ -142,43 +123,12 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
       if constexpr (RP) {
         if ((g + 1) % nt == 0) rope_offsets((g + 1) / nt);
       }
-      if constexpr (CG_LW_PF > 0) {
-        const int gp = g + CG_LW_PF;
-        uint32_t po = OOR;
-        if (gp < S) {
-          const int k = gp / nt, t = gp - k * nt;
-          int m0, n0;
-          tile_org(k, m0, n0);
-          po = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
-        }
-        char* scr = smem + bfp::SMEM + L * 256;
-#pragma unroll
-        for (int j = 0; j < bfl::LA; ++j)
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (bfw::lds_ptr_t)scr, 4, po == OOR ? OOR : po + va[j], 0, 0, 0);
-      }
-      if constexpr (CG_LW_RPF && (EPI & CG_EPI_RESID)) {
-        uint32_t ro = OOR;
-        if (g < S) {
-          const int k = g / nt, t = g - k * nt;
-          const int q = t * bfl::LWAVES + L;  // 64-line piece q of the tile's 1024 (256 rows x 4 lines)
-          if (q < 16) {
-            int m0, n0;
-            tile_org(k, m0, n0);
-            const int line = q * 64 + lane;
-            const int row = m0 + (line >> 2), col = n0 + (line & 3) * 32;
-            if (row < p.M && col < p.N) ro = (uint32_t)(((long long)row * p.ldr + col) * 4);
-          }
-        }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rres, (bfw::lds_ptr_t)(smem + bfp::SMEM + L * 256), 4, ro, 0, 0, 0);
-      }
     };
-    // residual prefetch ops per stage (1 with the fp32-residual epilogue under CG_LW_RPF)
-    constexpr int RPF = (CG_LW_RPF && (EPI & CG_EPI_RESID)) ? 1 : 0;
     if constexpr (RP) rope_offsets(0);
     issue(0);
     issue(1);
     for (int g = 0; g < S; ++g) {
-      wait_vm<bfl::PER_STAGE + 2 * bfl::PF_OPS + 2 * RPF>();  // stage g landed; stage g+1 may still be in flight
+      wait_vm<bfl::PER_STAGE>();  // stage g landed; stage g+1 may still be in flight
       __builtin_amdgcn_s_barrier();
       issue(g + 2);  // into the slot of stage g-1, whose reads retired before this barrier
     }
@@ -305,7 +255,7 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
 #pragma unroll
       for (int c = 0; c < 2; ++c)
         off_c[i][c] = (row < p.M && col[c] < p.N)
-                          ? (uint32_t)(((long long)row * p.ldc + ((RP && (CG_ROPE_DIAG & 8)) ? n0 + wn + 32 * c + 8 * g4 : col[c])) * ES)
+                          ? (uint32_t)(((long long)row * p.ldc + col[c]) * ES)
                           : OOR;
     }
     float bia[2][8];
@@ -383,14 +333,10 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
         const int row = m0 + wm + 16 * i + r16;
         const uint32_t t = (uint32_t)row % (uint32_t)p.rope_T;
         const uint32_t o = rot ? (t * (uint32_t)p.rope_half + (uint32_t)dim0) * 4u : OOR;
-        if (CG_ROPE_DIAG & 1) {
-          cq[i][0] = cq[i][1] = sq[i][0] = sq[i][1] = (u32x4){o, o, o, o};
-        } else {
-          cq[i][0] = bld(rcs, o);
-          cq[i][1] = bld(rcs, o + 16);
-          sq[i][0] = bld(rsn, o);
-          sq[i][1] = bld(rsn, o + 16);
-        }
+        cq[i][0] = bld(rcs, o);
+        cq[i][1] = bld(rcs, o + 16);
+        sq[i][0] = bld(rsn, o);
+        sq[i][1] = bld(rsn, o + 16);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -413,7 +359,6 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
         unpack_f32(sq[i][0], sq[i][1], sn);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          if (CG_ROPE_DIAG & 4) continue;
           const float c = rot ? cs[j] : 1.0f;
           const float y0 = fmaf(v0[j], c, -v1[j] * sn[j]);
           const float y1 = fmaf(v1[j], c, v0[j] * sn[j]);

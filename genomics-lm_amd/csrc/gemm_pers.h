@@ -72,13 +72,10 @@ __device__ __forceinline__ uint32_t b_src_off_swg(int pos, long long ld, int N) 
 __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
 }
-// epilogue store cache policy: 0 = default.  (16 = sc1, which drops the written line from the
-// XCD's L2, measured no faster on the C4 shapes: the output stream is not what evicts operands.)
-#ifndef CG_STORE_CPOL
-#define CG_STORE_CPOL 0
-#endif
+// epilogue stores with the default cache policy (sc1 and nt measured no faster / slower: the
+// outputs are re-read by the next product)
 __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, CG_STORE_CPOL);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 __device__ __forceinline__ void unpack_f32(u32x4 a, u32x4 b, float v[8]) {
   v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
@@ -113,33 +110,7 @@ __device__ __forceinline__ float dpp_sum16(float t) {
   t += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(t), 0x140, 0xF, 0xF, false));
   return t;
 }
-// diagnostic builds (timing only, results invalid): CG_PERS_DIAG=1 issues no operand DMAs after
-// the prologue, CG_PERS_DIAG=2 issues no MFMAs (fragment reads kept live)
-#ifndef CG_PERS_DIAG
-#define CG_PERS_DIAG 0
-#endif
-// timing-only diagnostic builds of the column-sum epilogue: 1 no DPP row sums, 2 no partial
-// stores (out-of-range offsets), 3 no accumulation
-// SwiGLU-backward epilogue operand loads in at most this many early pieces (0: all at the top of
-// the tile's last k-step)
-#ifndef CG_DSW_NP
-#define CG_DSW_NP 0
-#endif
-#ifndef CG_COLSUM_DIAG
-#define CG_COLSUM_DIAG 0
-#endif
-#ifndef CG_PERS_L2HOT
-#define CG_PERS_L2HOT 0
-#endif
-#if CG_PERS_DIAG == 2
-__device__ __forceinline__ v4f pmfma_diag(v8bf b, v8bf a, v4f c) {
-  asm volatile("" ::"v"(b), "v"(a));
-  return c;
-}
-#define PMFMA(b, a, c, x, y, z) bfp::pmfma_diag(b, a, c)
-#else
 #define PMFMA(b, a, c, x, y, z) __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, c, x, y, z)
-#endif
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -187,7 +158,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       ao = bo = OOR;
       return;
     }
-    const int k = g / nt, t = (CG_PERS_DIAG == 5 || CG_PERS_L2HOT) ? 0 : g - k * nt;  // diag 5: every step re-reads k-step 0 (L2-hot)
+    const int k = g / nt, t = g - k * nt;
     int m0, n0;
     tile_org(k, m0, n0);
     ao = (uint32_t)(((long long)m0 * p.lda + t * BKT) * 2);
@@ -295,11 +266,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       acc[i][j0 + 1] = PMFMA(bfr[0][j0 + 1], af[0][i], acc[i][j0 + 1], 0, 0, 0);
       if (gr < 4) af[1][gr] = bfg::frag<true>(as, wm + 16 * gr, 1, lane);
       else bfr[1][gr - 4] = bfrag(bs, wn, gr - 4, 1, lane);
-      if (CG_PERS_DIAG != 1) {
-        if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
-        else if (gr < A_CHUNKS + B_CHUNKS)
-          bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
-      }
+      if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
+      else if (gr < A_CHUNKS + B_CHUNKS)
+        bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -325,13 +294,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
   // step is followed by the epilogue, which must not hold 32 more registers).  Waits: the top one
   // as in `step`; the mid one (stage g+1 of step g) counts the ops issued after DMA(g+1): the
   // pieces / epilogue stores after step g-1 and this step's 6 DMAs.
-#ifndef CG_PERS_NO_PREFETCH
   // not for the fp32-residual and SwiGLU-backward epilogues: their piece registers plus the
   // prefetched fragments exceed 256 VGPRs (spills)
   constexpr bool PREF = !DSW && (EPI & CG_EPI_RESID) == 0;
-#else
-  constexpr bool PREF = false;
-#endif
   v8bf f0a[4], f0b[4];
   auto read_half0 = [&](int g) __attribute__((always_inline)) {
     const char* st = smem + (g % STAGES) * STAGE_BYTES;
@@ -363,11 +328,9 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       acc[i][j0 + 1] = PMFMA(f0b[j0 + 1], f0a[i], acc[i][j0 + 1], 0, 0, 0);
       if (gr < 4) af1[gr] = bfg::frag<true>(as, wm + 16 * gr, 1, lane);
       else bf1[gr - 4] = bfrag(bs, wn, gr - 4, 1, lane);
-      if (CG_PERS_DIAG != 1) {
-        if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
-        else if (gr < A_CHUNKS + B_CHUNKS)
-          bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
-      }
+      if (gr < A_CHUNKS) bfw::dma16(ra, nx + (wave + WAVES * gr) * 1024, ao + va[gr]);
+      else if (gr < A_CHUNKS + B_CHUNKS)
+        bfw::dma16(rb, nx + A_BYTES + (wave + WAVES * (gr - A_CHUNKS)) * 1024, bo + vb[gr - A_CHUNKS]);
     }
     if constexpr (MID) {
 #pragma unroll
@@ -550,7 +513,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] += r[j];
         }
-        if constexpr ((EPI & CG_EPI_COLSUM) != 0 && CG_COLSUM_DIAG != 3) {
+        if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
           const float keep = row < p.M ? 1.f : 0.f;
 #pragma unroll
           for (int j = 0; j < 8; ++j) csum[c][j] = fmaf(keep, v[j], csum[c][j]);
@@ -566,19 +529,15 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     if constexpr ((EPI & CG_EPI_COLSUM) != 0) {
       // sum over the 16 row lanes sharing these columns, then lane r16 == 0 writes the wave's
       // 64-row partial (every lane issues the stores; the others at an out-of-range offset)
-      if (CG_COLSUM_DIAG != 1) {
 #pragma unroll
-        for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            csum[c][j] = dpp_sum16(csum[c][j]);
-          }
-      }
+        for (int j = 0; j < 8; ++j) csum[c][j] = dpp_sum16(csum[c][j]);
       const int prow = (m0 + wm) >> 6;
       const __amdgpu_buffer_rsrc_t rw = rsrc(p.ws, (long long)((p.M + 63) >> 6) * p.N * 4);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        const uint32_t o = (CG_COLSUM_DIAG != 2 && r16 == 0 && col[c] < p.N) ? (uint32_t)(((long long)prow * p.N + col[c]) * 4) : OOR;
+        const uint32_t o = (r16 == 0 && col[c] < p.N) ? (uint32_t)(((long long)prow * p.N + col[c]) * 4) : OOR;
         bst(rw, o, (u32x4){__float_as_uint(csum[c][0]), __float_as_uint(csum[c][1]), __float_as_uint(csum[c][2]),
                            __float_as_uint(csum[c][3])});
         bst(rw, o + 16, (u32x4){__float_as_uint(csum[c][4]), __float_as_uint(csum[c][5]), __float_as_uint(csum[c][6]),
@@ -710,18 +669,10 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
       epilogue(k);
     }
   };
-  // diagnostic 3 (timing only: LDS hazards): waves 4-7 one barrier behind waves 0-3 (a stagger);
-  // 4: waves 4-7 at issue priority 1 for the whole kernel
-  if (CG_PERS_DIAG == 3 && wave >= 4) __builtin_amdgcn_s_barrier();
-  if (CG_PERS_DIAG == 4 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-#ifndef CG_PERS_NO_SPREAD
-  int np = NL == 0 ? 0 : nt >= 7 ? 4 : nt >= 5 ? 2 : nt >= 4 ? 1 : 0;
-#else
-  int np = 0;
-#endif
-  if constexpr (DSW) np = np > CG_DSW_NP ? CG_DSW_NP : np;
-  // DSW: 52 more VGPRs held over 5 steps spill (204 -> 256 + scratch); CG_DSW_NP caps its pieces
-  if constexpr (NL == 0 || (DSW && CG_DSW_NP == 0)) {
+  const int np = NL == 0 ? 0 : nt >= 7 ? 4 : nt >= 5 ? 2 : nt >= 4 ? 1 : 0;
+  // DSW: its operands in earlier pieces spill (52 more VGPRs held over 5 steps: 204 -> 256 +
+  // scratch; measured slower, round 4), so they load at the top of the tile's last k-step
+  if constexpr (NL == 0 || DSW) {
     tiles(std::integral_constant<int, 0>{});
   } else {
     if (np == 4) tiles(std::integral_constant<int, 4>{});
@@ -729,6 +680,5 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
     else if (np == 1) tiles(std::integral_constant<int, 1>{});
     else tiles(std::integral_constant<int, 0>{});
   }
-  if (CG_PERS_DIAG == 3 && wave < 4) __builtin_amdgcn_s_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
 }

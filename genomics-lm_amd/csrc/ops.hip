@@ -93,18 +93,12 @@ __device__ __forceinline__ void stw(bf16_t* p, const float* v) {
   else *(uint32_t*)p = u[0];
 }
 
-// LayerNorm row prefetch (env CG_LN_PF, bit set; unset = by measurement): 1 = the backward keeps
-// two rows in flight per wave, 2 = the forward runs 4 rows per wave with the next row's x loaded
-// before the current row's reductions.  rocprofv3 per kernel (profiles/round4/ln_prefetch.txt):
-// backward 23.88 -> 23.7 us at d 512, 34.39 -> 34.05 at d 384; forward 15.09 -> 14.11 at d 384
-// (W = 2) but 10.24 -> 10.44 at d 512 (W = 4), so the default takes the prefetching forward for
-// W = 2 rows only.
-static int g_ln_pf = [] {
-  const char* e = getenv("CG_LN_PF");
-  return e ? atoi(e) : -1;
-}();
-static inline bool ln_pf_bwd() { return g_ln_pf < 0 || (g_ln_pf & 1); }
-static inline bool ln_pf_fwd(int W) { return g_ln_pf < 0 ? W == 2 : (g_ln_pf & 2) != 0; }
+// LayerNorm row prefetch: the backward keeps two rows in flight per wave; the forward runs 4 rows
+// per wave with the next row's x loaded before the current row's reductions at W = 2 (d 384) only.
+// rocprofv3 per kernel (profiles/round4/ln_prefetch.txt): backward 23.88 -> 23.7 us at d 512,
+// 34.39 -> 34.05 at d 384; forward 15.09 -> 14.11 at d 384 (W = 2) but 10.24 -> 10.44 at d 512.
+static inline bool ln_pf_bwd() { return true; }
+static inline bool ln_pf_fwd(int W) { return W == 2; }
 
 // PF rows per wave of the prefetching forward
 constexpr int LN_FWD_RPW = 4;
@@ -271,15 +265,8 @@ extern "C" int cg_layernorm_bwd_blocks(int rows) {
   // 32 rows per block (8 per wave), at most 1024 blocks.  Round 2 measured 16 rows faster (C4:
   // 29.7 vs 38.2 us); with the round-2/3 kernel the two run alike (24.1 vs 24.5 us) and 32 halves
   // the partial rows the deferred column reduction reads (18.9 -> 14.9 us per group): C4 step
-  // -23..-46 us (3 interleaved same-box runs).  CG_LN_BWD_ROWS / CG_LN_BWD_MAXBLK: A/B switches.
-  static const int rpb = [] {
-    const char* e = getenv("CG_LN_BWD_ROWS");
-    return e && atoi(e) > 0 ? atoi(e) : 32;
-  }();
-  static const int maxb = [] {
-    const char* e = getenv("CG_LN_BWD_MAXBLK");
-    return e && atoi(e) > 0 ? atoi(e) : 1024;
-  }();
+  // -23..-46 us (3 interleaved same-box runs); 64 rows was slower again.
+  constexpr int rpb = 32, maxb = 1024;
   int b = cg_cdiv(rows, rpb);
   return b > maxb ? maxb : (b < 1 ? 1 : b);
 }
@@ -933,11 +920,7 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, flo
   hipStream_t s = (hipStream_t)stream;
   const uint32_t thr = drop_p > 0.f ? cg_drop_threshold(drop_p) : 0u;
   const float dscale = drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f;
-  static const int emb2 = [] {
-    const char* e = getenv("CG_EMB_TOK2");  // 0: the 64-column kernel (A/B switch)
-    return e ? atoi(e) : 1;
-  }();
-  if (dtok && emb2 && V <= EMB_V2 && d % 2 == 0 && ((uintptr_t)g & 7) == 0) {
+  if (dtok && V <= EMB_V2 && d % 2 == 0 && ((uintptr_t)g & 7) == 0) {
     const int nch = EMB_RCHUNKS2 > rows ? rows : EMB_RCHUNKS2;
     const size_t sh = (size_t)4 * V * 128 * sizeof(float);
     static bool attr2 = false;

@@ -80,41 +80,30 @@ typedef struct {
   /* CG_EPI_ROPE (ABI 0.3): tables and geometry */
   const float* rope_cos; const float* rope_sin;
   int rope_T, rope_hd, rope_heads;
+  /* ABI 0.4: kernel choice per call (the library holds no mutable process-wide settings).
+   * tile: CG_TILE_AUTO (0, what the engine uses) or a forced bf16 kernel for tests / A/B runs
+   * (CG_EUNSUPPORTED where it cannot run the product); max_wg: cap on the persistent grid
+   * (0 = one workgroup per CU; N > 0 = at most N workgroups, each walking more tiles). */
+  int tile, max_wg;
 } cg_gemm_desc;
+enum {
+  CG_TILE_AUTO = 0,    /* persistent 256x128 (loader-wave variant where measured faster), else    */
+                       /* 256x128 LDS-DMA tile for large K-contiguous products, else 128x128      */
+  CG_TILE_VEC = 1,     /* 128x128 register-staged tile                                           */
+  CG_TILE_WIDE = 2,    /* 256x128 LDS-DMA tile, one tile per workgroup                           */
+  CG_TILE_PERS = 3,    /* persistent 256x128, 8 waves issuing their own LDS-DMA (gemm_pers.h)    */
+  CG_TILE_PERS_LW = 4  /* persistent 256x128 with 4 dedicated loader waves (gemm_lw.h)           */
+};
 int cg_gemm(const cg_gemm_desc* d, void* stream);
-/* bf16 tile selection: -1 auto (default; env CG_GEMM_WIDE overrides at load), 0 = 128x128
- * register-staged tile only, 1 = 256x128 LDS-DMA tile whenever legal.  Returns the previous mode. */
-int cg_gemm_set_wide(int mode);
-/* persistent 256x128 tile for K-contiguous, un-split products (forward and dX): 1 = whenever
- * legal with one workgroup per CU (default; env CG_GEMM_PERS overrides at load), 0 = never,
- * N > 1 = whenever legal with the grid capped at N workgroups (each walks more tiles).
- * Returns the previous mode. */
-int cg_gemm_set_pers(int mode);
-/* CUs left free by the persistent launches (forward / dX tiles, grouped dW): they spread over
- * (CU count - reserve) workgroups; env CG_PERS_CU_RESERVE sets it at load.  Returns the previous
- * reserve.  cg_pers_cus: the CU count those launches (and the dW planner) use now. */
-int cg_set_cu_reserve(int n);
-/* persistent-tile variant with dedicated LDS-DMA loader waves (gemm_lw.h): 0 off, 1 (default; env
- * CG_PERS_LW at load) for the plain, bias, bias + GELU(') forward, fp32-residual and SwiGLU-forward
- * products (the RoPE epilogue always), 2 wherever it implements the epilogue.  Returns the previous
- * mode. */
-int cg_gemm_set_pers_lw(int mode);
-/* persistent-tile variant in which the two waves of each SIMD alternate MFMA and load segments
- * (gemm_pp.h): 0 off (default; env CG_PERS_PP at load), 1 for products without an epilogue or
- * with a bias only, 2 for every epilogue.  Takes precedence over the loader-wave variant.
- * Returns the previous mode. */
-int cg_gemm_set_pers_pp(int mode);
-/* 256x256-tile ping-pong variant (gemm_pp2.h) for bf16-output products with N >= 1024 and at
- * least one tile per CU: 0 off (default; env CG_PERS_PP2 at load), 1 on.  Returns the previous mode. */
-int cg_gemm_set_pers_pp2(int mode);
+/* the CU count the persistent launches (and the dW planner) spread over */
 int cg_pers_cus(void);
 
 /* Grouped weight-gradient GEMM: for every product p of the group
  *   C_p[n][k] (+)= alpha_p * sum_{m < K} A_p[m*lda_p + n] * B_p[m*ldb_p + k]
  * (dW = dY^T X of the nn.Linear call sites, A = dY and B = X both token-major bf16, C fp32).
  * Each output tile is reduced over all K rows inside one workgroup (no split-K partials);
- * the tiles of all products form one persistent launch (tile_m = 128 or 256 rows of C per
- * tile, 0 = default; env CG_DW_BM).  Any K >= 1 (a ragged last 64-row k-step is zero-filled);
+ * the tiles of all products form one persistent launch (tile_m codes: 128 = 128x128 (0 = this),
+ * 129 = the same with a 5-stage ring, 256 = 256x128, 512 = 256x256).  Any K >= 1 (a ragged last 64-row k-step is zero-filled);
  * N_out, K_out, lda, ldb % 8 == 0; ldc % 4. */
 #define CG_DW_MAX 32
 typedef struct {
@@ -133,12 +122,12 @@ typedef struct {
    * reduction launch adds them into C in slice order -- deterministic.  0 / 1 = no split. */
   int ksplit;
   float* workspace; size_t ws_bytes;
+  int max_wg; /* ABI 0.4: grid cap (0 = one workgroup per CU) */
 } cg_dw_group;
 int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream);
 size_t cg_gemm_dw_grouped_workspace(const cg_dw_group* grp);
-/* tiles one product contributes at tile_m (0 = current default); default tile_m setter */
+/* tiles one product contributes at tile_m */
 int cg_gemm_dw_tiles(int tile_m, int N_out, int K_out);
-int cg_gemm_dw_set_tile(int tile_m);
 
 /* LayerNorm (nn.LayerNorm, biased var, eps) -- model_tiny_gpt.py:137,139,216 */
 int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,
@@ -369,6 +358,24 @@ int cg_nonfinite_flag(const float* x, long long n, int* flag, void* stream);
  * loop.py:1067-1233).  Parameters live in ONE flat fp32 buffer whose layout is owned
  * by the library (cg_model_param_layout); grads use the same layout.
  * ----------------------------------------------------------------------------*/
+/* engine options (ABI 0.4): all zero = the defaults the engine was measured fastest with; each
+ * field selects a measured alternative for tests and same-box A/B runs.  They are part of the
+ * model's configuration (fixed for its lifetime), so the workspace size and the dW plan that
+ * cg_model_workspace_bytes / cg_model_dw_plan report are the ones forward / backward use. */
+typedef struct {
+  int dw_group;           /* blocks per grouped dW launch (0 = the planner's choice)            */
+  int dw_ksplit;          /* token-range split of the grouped dW tiles, 1..3 (0 = planner);     */
+                          /* out of range -> CG_EINVAL                                          */
+  int dw_remainder_first; /* 1: the short remainder dW group runs first from the top (0: last) */
+  int head_dw_separate;   /* 1: the tied head's dW as its own split-K product in backward phase */
+                          /* 0 (0: inside the first grouped dW launch)                          */
+  int rope_tables;        /* 1: RoPE as separate cg_rope_tab passes (0: fused into the qkv      */
+                          /* projection's epilogue and the attention backward)                  */
+  int attn_mask_kernel;   /* 1: the attention dropout keep bits by cg_attn_drop_mask before     */
+                          /* each block's forward (0: written by the attention forward itself)  */
+  int dw_plan_tokens;     /* > 0: plan the grouped dW as for steps of this many tokens (a small  */
+                          /* parity step then runs a large step's plan); 0: the step's own B*T  */
+} cg_model_opts;
 typedef struct {
   int vocab_size, block_size, n_layer, n_head, n_kv_head, n_embd;
   int use_swiglu, use_rope, sep_id /* <0: none */, tie_embeddings;
@@ -376,6 +383,7 @@ typedef struct {
   int n_offsets; int offsets[8];
   float dropout, label_smoothing, ln_eps;
   int dtype; /* CG_F32 or CG_BF16 */
+  cg_model_opts opts;
 } cg_model_cfg;
 
 /* parameter tensor kinds (layer = -1 for global tensors) */
@@ -396,9 +404,10 @@ typedef struct {
 int cg_model_param_layout(const cg_model_cfg* cfg, cg_param_entry* out, int max,
                           long long* total_elems);
 size_t cg_model_workspace_bytes(const cg_model_cfg* cfg, int B, int T);
-/* the grouped weight-gradient plan of the bf16 engine: blocks per grouped dW launch and the
- * tile rows (128 or 256) chosen for this configuration on the current device */
-int cg_model_dw_plan(const cg_model_cfg* cfg, int* group_layers, int* tile_m);
+/* the grouped weight-gradient plan of the bf16 engine for a (B, T) step on the current device:
+ * blocks per grouped dW launch, the tile code of a full group and its token-range split (the plan
+ * forward / backward use at that B * T; it depends on the token count) */
+int cg_model_dw_plan(const cg_model_cfg* cfg, int B, int T, int* group_layers, int* tile_m, int* ksplit);
 
 typedef struct {
   cg_model_cfg cfg;
@@ -439,9 +448,6 @@ typedef struct {
   /* engine-private: the parameter / bias gradient column reductions deferred to the end of the
    * current dW group (one cg_reduce_columns launch per group) */
   cg_reduce_batch reduce_pending;
-  /* engine-private: the embedding backward already ran inside phase 1 of block 0 (overlapped
-   * with the last dW group), so phase 2 skips it */
-  int embed_done;
 } cg_model;
 
 /* forward: logits (fp32 [B*T][V] contiguous; NULL => internal buffer), loss (device
@@ -524,38 +530,18 @@ int cg_probe_bytes(double* bytes);
  * all-reduce) when measuring the persistent launches' sensitivity to busy CUs */
 int cg_diag_occupy(int n_cus, int usec, void* stream);
 
-/* the tied head's weight gradient (bf16, tied, no aux heads) deferred from backward phase 0
- * into the first grouped dW launch: 1 (default; env CG_HEAD_DW_DEFER at load) or 0 (a split-K
- * product in phase 0).  Returns the previous setting. */
-int cg_set_head_dw_defer(int on);
-/* RoPE models: 1 (default; env CG_ROPE_FUSED at load) rotates inside the qkv projection's GEMM
- * epilogue (CG_EPI_ROPE) and the attention backward (cg_attn_bwd_rope), 0 uses the separate
- * cg_rope_tab passes.  Returns the previous setting. */
-int cg_set_rope_fused(int on);
-/* grouped dW plan controls (read when a backward starts; change them only between steps):
- * cg_set_dw_order 1 = the short remainder group last from the top (default; env CG_DW_ORDER),
- * 0 = first; cg_set_dw_group(n) forces n blocks per group (0 = planner's choice; env
- * CG_DW_GROUP); cg_set_dw_ksplit(k) forces a k-way token-range split of every group's tiles
- * (1..3; 0 = planner's choice; env CG_DW_KSPLIT) -- set it before the model's first step at a
- * (B, T), which sizes the slab workspace.  All return the previous setting. */
-int cg_set_dw_order(int order);
-int cg_set_dw_group(int blocks);
-int cg_set_dw_ksplit(int ks);
-/* 1 (env CG_DW_OVERLAP): the last dW group of a backward runs on a per-device side stream beside
- * block 0's LayerNorm backward, the deferred reductions and the embedding backward, joined before
- * phase 1 of block 0 returns; 0 (default, measured faster) = all on the caller's stream.  Returns
- * the previous setting. */
-int cg_set_dw_overlap(int on);
-
 /* sizeof the named ABI struct ("cg_gemm_desc", "cg_dw_product", "cg_dw_group", "cg_reduce_job",
  * "cg_reduce_batch", "cg_transpose_item", "cg_transpose_batch", "cg_adamw_segment",
- * "cg_model_cfg", "cg_param_entry", "cg_model"), 0 for another name: lets a binding that mirrors
+ * "cg_model_cfg", "cg_param_entry", "cg_model", "cg_model_opts"), 0 for another name: lets a binding that mirrors
  * the layouts check them against the library it loaded. */
 size_t cg_struct_bytes(const char* name);
 
 /* "codonlm_hip <abi> gfx950".  ABI 0.2 (round 3): cg_gemm_desc.ws_bytes and the size_t
  * workspace-size argument after every workspace pointer.  ABI 0.3 (round 4): cg_model gained
- * the engine-private head_dw_* fields at its end. */
+ * the engine-private head_dw_* fields at its end.  ABI 0.4 (round 5): no process-wide setters --
+ * cg_gemm_desc.tile / max_wg, cg_dw_group.max_wg and cg_model_cfg.opts replace the cg_set_* /
+ * cg_gemm_set_* calls and the environment switches; cg_model_dw_plan takes (B, T) and reports the
+ * token split; cg_model.embed_done is gone. */
 const char* cg_version(void);
 
 #ifdef __cplusplus

@@ -36,7 +36,7 @@ def test_ctypes_struct_mirrors_match_the_library():
                "cg_reduce_job": L.ReduceJob, "cg_reduce_batch": L.ReduceBatch,
                "cg_transpose_item": L.TransposeItem, "cg_transpose_batch": L.TransposeBatch,
                "cg_adamw_segment": L.AdamwSegment, "cg_model_cfg": L.ModelCfg,
-               "cg_param_entry": L.ParamEntry, "cg_model": L.Model}
+               "cg_param_entry": L.ParamEntry, "cg_model": L.Model, "cg_model_opts": L.ModelOpts}
     for name, cls in mirrors.items():
         assert L.lib.cg_struct_bytes(name.encode()) == ctypes.sizeof(cls), name
     assert L.lib.cg_struct_bytes(b"nope") == 0

@@ -2,8 +2,11 @@
 
 The reference-produced goldens keep PyTorch's default N(0, 1) embeddings, so with the tied head
 their logits are tens apart and no near-tie ever occurs (minimum top-2 margins 6.7-236 logits).
-Here the embeddings are drawn at a trained-model scale (std 0.02) so the logits of the C2 / C4
-geometries are O(0.5) and the top-2 margins of ~1000 positions reach 1e-4 .. 1e-5.  The fp32
+Here the embeddings are drawn at a trained-model scale (std 0.02) so the logits of the C2 / C3 /
+C4 / C5 geometries are O(0.5) and the top-2 margins of ~1000 positions reach 1e-4 .. 1e-5.  C3 is
+the geometry a user queries (GQA4 + RoPE + SwiGLU, hd 48, bench_b8_gqa4.yaml); C5 carries the
+five multi-offset heads, whose argmax is checked at every position too (the tied head applied to
+each offset projection, model_tiny_gpt.py:329-337).  The fp32
 engine must give the oracle's argmax (the reference's greedy pick, query_model.py:163-182 /
 generate.py:13-27) at every position except where the oracle's own margin is below 2x the run's
 measured max |dlogit|; the test prints how many positions that exempts (expected: ~0) next to the
@@ -20,10 +23,32 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 GEOM = {
-    # SURVEY §8 C2 / C4 shapes (fewer layers at C4 keep the CPU oracle to seconds)
+    # SURVEY §8 C2 - C5 shapes (fewer layers at C3 / C4 / C5 keep the CPU oracle to seconds)
     "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, B=2),
+    "c3": dict(n_layer=4, n_head=8, n_kv_head=4, n_embd=384, block_size=512, use_swiglu=True, use_rope=True, B=2),
     "c4": dict(n_layer=4, n_head=8, n_embd=512, block_size=1024, B=1),
+    "c5": dict(n_layer=4, n_head=8, n_embd=384, block_size=512, termination_aux=True,
+               multi_offset_targets=[2, 4, 8, 16, 32], B=2),
 }
+
+
+def _check(tag, got, ref, need_ties=True):
+    """argmax of got == argmax of ref except where ref's top-2 margin <= 2 x the measured max
+    |dlogit|; prints the counts.  Returns max |dlogit| / logit scale."""
+    maxd = float(np.abs(got - ref).max())
+    scale = float(np.abs(ref).max())
+    srt = np.sort(ref, axis=-1)
+    margin = srt[..., -1] - srt[..., -2]
+    diff = got.argmax(-1) != ref.argmax(-1)
+    exempt = margin <= 2 * maxd
+    print(f"{tag}: {margin.size} positions, logit scale {scale:.3g}, max |dlogit| {maxd:.3g} "
+          f"(rel {maxd / max(scale, 1e-30):.3g}), min top-2 margin {margin.min():.3g}, "
+          f"margins < 1e-3: {int((margin < 1e-3).sum())}, exempted (margin <= 2 max|dlogit|): {int(exempt.sum())}, "
+          f"argmax differences: {int(diff.sum())}")
+    if need_ties:  # the test is only meaningful if near-ties occur at all
+        assert margin.min() < 1e-3, tag
+    assert maxd <= 1e-4 * max(1.0, scale), tag
+    assert not np.any(diff & ~exempt), (tag, np.argwhere(diff & ~exempt)[:8])
 
 
 def _tokens(B, T, seed):
@@ -45,27 +70,28 @@ def test_greedy_ids_at_near_ties(geom):
     cfg = O.OracleConfig(vocab_size=68, dropout=0.0, label_smoothing=0.0, **gd)
     params = O.synthetic_params(cfg, seed=11)
     for k in ("tok_emb.weight", "pos_emb.weight"):
-        params[k] = (0.02 * params[k]).astype(np.float32)
+        if k in params:
+            params[k] = (0.02 * params[k]).astype(np.float32)
     m = TinyGPT(68, cfg.block_size, n_layer=cfg.n_layer, n_head=cfg.n_head, n_embd=cfg.n_embd, dropout=0.0,
+                n_kv_head=cfg.n_kv_head, use_swiglu=cfg.use_swiglu, use_rope=cfg.use_rope,
+                termination_aux=cfg.termination_aux, multi_offset_targets=cfg.multi_offset_targets or None,
                 compute_dtype="fp32", device=DEV)
     missing, unexpected = m.load_state_dict({k: torch.from_numpy(v) for k, v in params.items()}, strict=False)
     assert not unexpected
     m.eval()
     idx = _tokens(B, cfg.block_size, seed=5)
+    aux = bool(cfg.multi_offset_targets)
     with torch.no_grad():
-        got = m(torch.from_numpy(idx).to(DEV))[0].float().cpu().numpy()
-        ref = O.forward(cfg, params, idx)["logits"].numpy()
-    maxd = float(np.abs(got - ref).max())
-    scale = float(np.abs(ref).max())
-    srt = np.sort(ref, axis=-1)
-    margin = srt[..., -1] - srt[..., -2]
-    diff = got.argmax(-1) != ref.argmax(-1)
-    exempt = margin <= 2 * maxd
-    print(f"{geom}: {margin.size} positions, logit scale {scale:.3g}, max |dlogit| {maxd:.3g} "
-          f"(rel {maxd / max(scale, 1e-30):.3g}), min top-2 margin {margin.min():.3g}, "
-          f"margins < 1e-3: {int((margin < 1e-3).sum())}, exempted (margin <= 2 max|dlogit|): {int(exempt.sum())}, "
-          f"argmax differences: {int(diff.sum())}")
-    # the test is only meaningful if near-ties occur at all
-    assert margin.min() < 1e-3
-    assert maxd <= 1e-4 * max(1.0, scale)
-    assert not np.any(diff & ~exempt), np.argwhere(diff & ~exempt)[:8]
+        if aux:
+            lg, _, gaux = m(torch.from_numpy(idx).to(DEV), return_aux=True)
+        else:
+            lg = m(torch.from_numpy(idx).to(DEV))[0]
+        got = lg.float().cpu().numpy()
+        o = O.forward(cfg, params, idx)
+        ref = o["logits"].numpy()
+    _check(geom, got, ref)
+    if aux:  # every offset head's greedy pick (the tied head over its projection)
+        for k, r in o["aux"]["offset_logits"].items():
+            _check(f"{geom} offset {k}", gaux["offset_logits"][k].float().cpu().numpy(), r.numpy(), need_ties=False)
+        _check(f"{geom} termination", gaux["termination_logits"].float().cpu().numpy(),
+               o["aux"]["termination_logits"].numpy(), need_ties=False)

@@ -3,6 +3,7 @@
 Every test here needs the MI355X (marker ``gpu``) and calls through the C-ABI
 (libcodonlm_hip.so) via codonlm_amd.ops.
 """
+import functools
 import math
 
 import numpy as np
@@ -186,23 +187,20 @@ def test_swiglu_fwd_bwd(dtype, H, Hp, ld_pad):
     assert torch.all(d[:, H:Hp] == 0) and torch.all(d[:, Hp + H:] == 0)
 
 
-@pytest.mark.parametrize("pp", [0, 2])
+@pytest.mark.parametrize("tile", [0, 3])
 @pytest.mark.parametrize("M,Hp,H,K", [(1024, 1024, 1024, 384), (700, 1408, 1365, 512), (256, 128, 100, 128)])
-def test_gemm_swiglu_epilogues(M, Hp, H, K, pp):
+def test_gemm_swiglu_epilogues(M, Hp, H, K, tile):
     """The gate|up product with SwiGLU in the persistent tile's epilogue (CG_EPI_SWIGLU: B rows
     remapped so one lane holds gate j and up j) and the dL/ds product with the SwiGLU backward in
     its epilogue (CG_EPI_DSWIGLU), against the separate passes (cg_swiglu_fwd / _bwd) on the same
-    bf16 products."""
+    bf16 products.  tile 0: automatic (the forward on the loader-wave kernel); 3 = CG_TILE_PERS:
+    both on the eight-wave kernel."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
-    old_pp = L.lib.cg_gemm_set_pers_pp(pp)
-    try:
-        _swiglu_epilogues(ops, L, M, Hp, H, K)
-    finally:
-        L.lib.cg_gemm_set_pers_pp(old_pp)
+    _swiglu_epilogues(ops, L, M, Hp, H, K, tile)
 
 
-def _swiglu_epilogues(ops, L, M, Hp, H, K):
+def _swiglu_epilogues(ops, L, M, Hp, H, K, tile=0):
     g = torch.Generator().manual_seed(M + Hp)
     x = (torch.randn(M, K, generator=g) * 0.5).to(DEV, torch.bfloat16)
     wgu = torch.randn(2 * Hp, K, generator=g) * K ** -0.5
@@ -212,7 +210,7 @@ def _swiglu_epilogues(ops, L, M, Hp, H, K):
     gu_ref = ops.gemm(x, wgu)                                  # [M][2Hp]
     s_ref = ops.swiglu_fwd(gu_ref, H)
     gu = torch.full((M, 2 * Hp), float("nan"), device=DEV, dtype=torch.bfloat16)
-    s = ops.gemm(x, wgu, N=Hp, epilogue=L.EPI_SWIGLU, aux_out=gu, n_valid=H)
+    s = ops.gemm(x, wgu, N=Hp, epilogue=L.EPI_SWIGLU, aux_out=gu, n_valid=H, tile=tile)
     torch.cuda.synchronize()
     assert torch.equal(gu, gu_ref)  # same products, same k order: bitwise
     # s from the unrounded fp32 g, u (the separate pass reads them in bf16): bf16-rounding close
@@ -226,7 +224,7 @@ def _swiglu_epilogues(ops, L, M, Hp, H, K):
     ds = ops.gemm(gin, wdT)                                    # [M][Hp]
     dgu_ref = ops.swiglu_bwd(gu_ref, ds, H)
     dgu = torch.full((M, 2 * Hp), float("nan"), device=DEV, dtype=torch.bfloat16)
-    ops.gemm(gin, wdT, N=Hp, out=dgu, epilogue=L.EPI_DSWIGLU, aux=gu_ref, n_valid=H)
+    ops.gemm(gin, wdT, N=Hp, out=dgu, epilogue=L.EPI_DSWIGLU, aux=gu_ref, n_valid=H, tile=tile)
     torch.cuda.synchronize()
     # same fp32 product, dgu computed from it before rounding (the separate pass reads ds in
     # bf16): equal to bf16 rounding
@@ -715,7 +713,8 @@ def test_adamw_offset_views(shift):
 @pytest.mark.parametrize("ak,bk", [(1, 1), (1, 0), (0, 0), (0, 1)])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 512), (1000, 200, 192), (256, 136, 1024)])
 def test_gemm_wide_tile(mode, ak, bk, M, N, K):
-    """The 256x128 LDS-DMA tile (forced on) against fp32, incl. partial M/N tiles and split-K."""
+    """The 256x128 LDS-DMA tile (mode 1: CG_TILE_WIDE) and the 128x128 register-staged tile (mode 0:
+    CG_TILE_VEC) against fp32, incl. partial M/N tiles and split-K, every operand layout."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
     g = torch.Generator().manual_seed(M + N + K + 10 * ak + bk)
@@ -725,16 +724,13 @@ def test_gemm_wide_tile(mode, ak, bk, M, N, K):
     a = (Am if ak else Am.t().contiguous()).to(DEV, torch.bfloat16)
     b = (Bn if bk else Bn.t().contiguous()).to(DEV, torch.bfloat16)
     ref = _bf(Am) @ _bf(Bn).t()
-    old = L.lib.cg_gemm_set_wide(mode)
-    try:
-        out = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32)
-        outb = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.bfloat16,
-                        bias=bias.to(DEV), epilogue=L.EPI_BIAS)
-        outs = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32,
-                        split_k=2)
-        torch.cuda.synchronize()
-    finally:
-        L.lib.cg_gemm_set_wide(old)
+    t = L.TILE_WIDE if mode else L.TILE_VEC
+    out = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32, tile=t)
+    outb = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.bfloat16,
+                    bias=bias.to(DEV), epilogue=L.EPI_BIAS, tile=t)
+    outs = ops.gemm(a, b, a_kcontig=bool(ak), b_kcontig=bool(bk), M=M, N=N, K=K, out_dtype=torch.float32,
+                    split_k=2, tile=t)
+    torch.cuda.synchronize()
     tol = 2e-2 * math.sqrt(K)
     assert (out.cpu() - ref).abs().max().item() <= tol
     assert (outs.cpu() - ref).abs().max().item() <= tol
@@ -751,7 +747,7 @@ def test_transpose16_batch():
         assert torch.equal(o.cpu(), m.cpu().t())
 
 
-@pytest.mark.parametrize("lw", [0, 1, 2, 3])
+@pytest.mark.parametrize("lw", [0, 1, 2])
 @pytest.mark.parametrize("cap", [1, 3])
 @pytest.mark.parametrize("M,N,K", [(600, 200, 192), (1000, 264, 128), (512, 384, 256), (600, 200, 320),
                                    (520, 264, 512)])
@@ -761,8 +757,9 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     and the counted waits carry across tile boundaries with epilogue stores in flight.  K = 128 /
     192 issue the epilogue loads in the last k-step; K = 256 / 320 / 512 spread them over the
     tile's last 1 / 2 / 4 k-steps.  CG_EPI_GELU_DERIV: the forward stores gelu'(pre) and the
-    backward multiplies by it.  lw=2: the same on the loader-wave variant (gemm_lw.h) for every
-    epilogue it implements.  lw=3: the ping-pong variant (gemm_pp.h) for every epilogue."""
+    backward multiplies by it.  lw=0: the eight-wave kernel (CG_TILE_PERS) for every epilogue;
+    lw=1: automatic (each epilogue on the kernel the engine uses); lw=2: the loader-wave variant
+    (gemm_lw.h, CG_TILE_PERS_LW) for every epilogue it implements."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
     g = torch.Generator().manual_seed(M + N + K)
@@ -773,39 +770,33 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     xd, wd = x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16)
     base = _bf(x) @ _bf(w).t()
     tol = 3e-2 * 4
-    old = L.lib.cg_gemm_set_pers(cap)
-    old_lw = L.lib.cg_gemm_set_pers_lw(lw if lw < 3 else 0)
-    old_pp = L.lib.cg_gemm_set_pers_pp(2 if lw == 3 else 0)
-    try:
-        y0 = ops.gemm(xd, wd, out_dtype=torch.float32)
-        y0b = ops.gemm(xd, wd, out_dtype=torch.bfloat16)
-        yb = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV), epilogue=L.EPI_BIAS)
-        yr = ops.gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
-                      epilogue=L.EPI_BIAS | L.EPI_RESID)
-        aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        yg = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV), epilogue=L.EPI_BIAS | L.EPI_GELU,
-                      aux_out=aux)
-        ydg = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux)
-        p, seed = 0.25, 777
-        ydr = ops.gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
-                       epilogue=L.EPI_BIAS | L.EPI_DROPOUT | L.EPI_RESID, drop_seed=seed, drop_p=p)
-        acc0 = torch.randn(M, N, generator=g)
-        yac = acc0.clone().to(DEV)
-        ops.gemm(xd, wd, out=yac, epilogue=L.EPI_ACCUM, alpha=0.5)
-        cs = torch.empty(N, device=DEV)
-        ydc = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux, colsum_out=cs)
-        auxd = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-        ygd = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV),
-                       epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_DERIV, aux_out=auxd)
-        ydgd = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=auxd)
-        csd = torch.empty(N, device=DEV)
-        ydcd = ops.gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=auxd,
-                        colsum_out=csd)
-        torch.cuda.synchronize()
-    finally:
-        L.lib.cg_gemm_set_pers(old)
-        L.lib.cg_gemm_set_pers_lw(old_lw)
-        L.lib.cg_gemm_set_pers_pp(old_pp)
+    gemm = functools.partial(ops.gemm, tile=(L.TILE_PERS, L.TILE_AUTO, L.TILE_PERS_LW)[lw],
+                             max_wg=cap if cap > 1 else 0)
+    y0 = gemm(xd, wd, out_dtype=torch.float32)
+    y0b = gemm(xd, wd, out_dtype=torch.bfloat16)
+    yb = gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV), epilogue=L.EPI_BIAS)
+    yr = gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
+                  epilogue=L.EPI_BIAS | L.EPI_RESID)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    yg = gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV), epilogue=L.EPI_BIAS | L.EPI_GELU,
+                  aux_out=aux)
+    ydg = gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux)
+    p, seed = 0.25, 777
+    ydr = gemm(xd, wd, out_dtype=torch.float32, bias=bias.to(DEV), resid=res.to(DEV),
+                   epilogue=L.EPI_BIAS | L.EPI_DROPOUT | L.EPI_RESID, drop_seed=seed, drop_p=p)
+    acc0 = torch.randn(M, N, generator=g)
+    yac = acc0.clone().to(DEV)
+    gemm(xd, wd, out=yac, epilogue=L.EPI_ACCUM, alpha=0.5)
+    cs = torch.empty(N, device=DEV)
+    ydc = gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux, colsum_out=cs)
+    auxd = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ygd = gemm(xd, wd, out_dtype=torch.bfloat16, bias=bias.to(DEV),
+                   epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_DERIV, aux_out=auxd)
+    ydgd = gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=auxd)
+    csd = torch.empty(N, device=DEV)
+    ydcd = gemm(xd, wd, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=auxd,
+                    colsum_out=csd)
+    torch.cuda.synchronize()
     pre = base + bias
     assert (y0.cpu() - base).abs().max() < tol
     assert (y0b.float().cpu() - base).abs().max() < tol + 0.01 * base.abs().max()
@@ -834,63 +825,6 @@ def test_gemm_persistent_tile_epilogues(cap, M, N, K, lw):
     assert (csd.cpu() - ref_dgd.sum(0)).abs().max() < 1e-2 * (1 + ref_dgd.abs().sum(0).max())
 
 
-@pytest.mark.parametrize("cap", [1, 3])
-@pytest.mark.parametrize("M,N,K", [(8192, 2048, 512), (8000, 2100, 128), (4096, 4160, 256)])
-def test_gemm_pp2_epilogues(cap, M, N, K):
-    """The 256x256 ping-pong tile (gemm_pp2.h; N >= 1024, at least one tile per CU) for every
-    epilogue it implements, partial M / N tiles, K = 128 / 256 / 512 (4 / 8 / 16 k-steps of 32),
-    and (cap = 3) three workgroups that each walk ~100 tiles, so the 4-stage ring and its counted
-    waits cross many tile seams with epilogue stores in flight.  Each result against the
-    persistent 256x128 tile on the same bf16 operands (same fp32 products, different summation
-    order) and fp32 torch."""
-    ops = _ops()
-    L = __import__("codonlm_amd._lib", fromlist=["x"])
-    g = torch.Generator().manual_seed(M + N + K)
-    x = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
-    w = (torch.randn(N, K, generator=g) * K ** -0.5).to(DEV, torch.bfloat16)
-    bias = torch.randn(N, generator=g).to(DEV)
-    aux = (torch.randn(M, N, generator=g) * 0.5).to(DEV, torch.bfloat16)
-
-    def run(pp2):
-        old = L.lib.cg_gemm_set_pers(cap)
-        old2 = L.lib.cg_gemm_set_pers_pp2(pp2)
-        try:
-            out = {}
-            out["plain"] = ops.gemm(x, w, out_dtype=torch.bfloat16)
-            out["bias"] = ops.gemm(x, w, out_dtype=torch.bfloat16, bias=bias, epilogue=L.EPI_BIAS)
-            a1 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            out["gelu"] = ops.gemm(x, w, out_dtype=torch.bfloat16, bias=bias, epilogue=L.EPI_BIAS | L.EPI_GELU,
-                                   aux_out=a1)
-            out["gelu_pre"] = a1
-            a2 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
-            out["gelud"] = ops.gemm(x, w, out_dtype=torch.bfloat16, bias=bias,
-                                    epilogue=L.EPI_BIAS | L.EPI_GELU | L.EPI_GELU_DERIV, aux_out=a2)
-            out["gelud_d"] = a2
-            out["dgelu"] = ops.gemm(x, w, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU, aux=aux)
-            out["dgelud"] = ops.gemm(x, w, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=aux)
-            cs = torch.empty(N, device=DEV)
-            out["dgeludc"] = ops.gemm(x, w, out_dtype=torch.bfloat16, epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV,
-                                      aux=aux, colsum_out=cs)
-            out["cs"] = cs
-            cs2 = torch.empty(N, device=DEV)
-            out["plainc"] = ops.gemm(x, w, out_dtype=torch.bfloat16, colsum_out=cs2)
-            out["cs2"] = cs2
-            torch.cuda.synchronize()
-            return out
-        finally:
-            L.lib.cg_gemm_set_pers(old)
-            L.lib.cg_gemm_set_pers_pp2(old2)
-
-    got, ref = run(1), run(0)
-    base = x.float() @ w.float().t()
-    assert (got["plain"].float() - base).abs().max().item() <= 2e-2 * (1 + base.abs().max().item())
-    for key in got:
-        a, b = got[key].float(), ref[key].float()
-        tol = 1e-3 if key in ("cs", "cs2") else 1.6e-2
-        err = (a - b).abs().max().item()
-        assert err <= tol * (1 + b.abs().max().item()), (key, err)
-
-
 @pytest.mark.parametrize("dtype,pers", [(torch.float32, 1), (torch.bfloat16, 0), (torch.bfloat16, 1)])
 def test_gemm_colsum_epilogue(dtype, pers):
     """CG_EPI_COLSUM (fused bias-gradient column sums) on the persistent tile and on the
@@ -902,13 +836,10 @@ def test_gemm_colsum_epilogue(dtype, pers):
     x = torch.randn(M, K, generator=g)
     w = torch.randn(N, K, generator=g) * 0.1
     base = (_bf(x) @ _bf(w).t()) if dtype == torch.bfloat16 else x @ w.t()
-    old = L.lib.cg_gemm_set_pers(pers)
-    try:
-        cs = torch.empty(N, device=DEV)
-        y = ops.gemm(x.to(DEV, dtype), w.to(DEV, dtype), out_dtype=dtype, colsum_out=cs)
-        torch.cuda.synchronize()
-    finally:
-        L.lib.cg_gemm_set_pers(old)
+    cs = torch.empty(N, device=DEV)
+    y = ops.gemm(x.to(DEV, dtype), w.to(DEV, dtype), out_dtype=dtype, colsum_out=cs,
+                 tile=L.TILE_AUTO if pers else L.TILE_VEC)
+    torch.cuda.synchronize()
     tol = 1e-3 if dtype == torch.float32 else 2e-2
     assert (y.float().cpu() - base).abs().max() < tol * 4 * (1 + base.abs().max())
     assert (cs.cpu() - base.sum(0)).abs().max() < tol * (1 + base.abs().sum(0).max())
@@ -944,16 +875,14 @@ def test_gemm_rope_epilogue(cap, M, K, T, H, KV, hd, extra):
     ref_rot = torch.cat([torch.cat([a * c - b * s, b * c + a * s], -1).reshape(M, nq), ref[:, nq:]], 1)
     xd, wd, bd = x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16), bias.to(DEV)
     cd, sd = cos.to(DEV), sin.to(DEV)
-    old = L.lib.cg_gemm_set_pers(cap)
-    try:
-        fused = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bd, epilogue=L.EPI_BIAS, rope=(cd, sd, T, hd, H + KV))
-        plain = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bd, epilogue=L.EPI_BIAS)
-        unf = plain.clone()
-        if M % T == 0:
-            ops.rope_(unf, M // T, T, H, KV, hd, cd, sd)
-        torch.cuda.synchronize()
-    finally:
-        L.lib.cg_gemm_set_pers(old)
+    mw = cap if cap > 1 else 0
+    fused = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bd, epilogue=L.EPI_BIAS, rope=(cd, sd, T, hd, H + KV),
+                     max_wg=mw)
+    plain = ops.gemm(xd, wd, out_dtype=torch.bfloat16, bias=bd, epilogue=L.EPI_BIAS, max_wg=mw)
+    unf = plain.clone()
+    if M % T == 0:
+        ops.rope_(unf, M // T, T, H, KV, hd, cd, sd)
+    torch.cuda.synchronize()
     ff = fused.float().cpu()
 
     def rel(u, v):
@@ -968,7 +897,7 @@ def test_gemm_rope_epilogue(cap, M, K, T, H, KV, hd, extra):
 
 def test_gemm_rope_epilogue_unsupported():
     """CG_EPI_ROPE outside the loader-wave tile is CG_EUNSUPPORTED (the engine then keeps the
-    cg_rope_tab pass): fp32 operands, hd % 16 != 0, loader waves off."""
+    cg_rope_tab pass): fp32 operands, hd % 16 != 0, the eight-wave kernel forced."""
     ops = _ops()
     L = __import__("codonlm_amd._lib", fromlist=["x"])
     cos, sin = _rope_tabs(64, 40)
@@ -980,12 +909,8 @@ def test_gemm_rope_epilogue_unsupported():
     with pytest.raises(ValueError, match="CG_EUNSUPPORTED"):
         ops.gemm(xb, wb, rope=(cos.to(DEV), sin.to(DEV), 64, 40, 8))
     c2, s2 = _rope_tabs(64, 32)
-    old = L.lib.cg_gemm_set_pers_lw(0)
-    try:
-        with pytest.raises(ValueError, match="CG_EUNSUPPORTED"):
-            ops.gemm(xb, wb[:256], rope=(c2.to(DEV), s2.to(DEV), 64, 32, 4))
-    finally:
-        L.lib.cg_gemm_set_pers_lw(old)
+    with pytest.raises(ValueError, match="CG_EUNSUPPORTED"):
+        ops.gemm(xb, wb[:256], rope=(c2.to(DEV), s2.to(DEV), 64, 32, 4), tile=L.TILE_PERS)
 
 
 @pytest.mark.parametrize("B,T,H,KV,hd,window,p", [(2, 1024, 8, 8, 64, 0, 0.1), (2, 512, 8, 4, 48, 0, 0.0),

@@ -29,25 +29,29 @@ from codonlm_amd import TinyGPT, _lib as L  # noqa: E402
 from codonlm_amd.optim import FusedAdamW  # noqa: E402
 from codonlm_amd.training.ddp import bucket_ranges  # noqa: E402
 
-PLANS = [("2/5/5", 0, 0), ("5/5/2", 1, 0), ("4/4/4", 0, 4), ("6/6", 0, 6)]
+# (name, engine_opts): the dW group plans (cg_model_opts dw_remainder_first / dw_group)
+PLANS = [("2/5/5", {"dw_remainder_first": 1}), ("5/5/2", {}), ("4/4/4", {"dw_remainder_first": 1, "dw_group": 4}),
+         ("6/6", {"dw_remainder_first": 1, "dw_group": 6})]
 
 
 def main():
     busbws = [float(a) for a in sys.argv[1:]] or [300.0, 600.0]
     dev = torch.device("cuda", 0)
-    torch.manual_seed(0)
-    m = TinyGPT(68, 1024, n_layer=12, n_head=8, n_embd=512, dropout=0.1, label_smoothing=0.05,
-                compute_dtype="bf16", device=dev)
-    m.train()
-    opt = FusedAdamW(m, lr=3e-4, weight_decay=0.05)
+    models = {}
+    for name, opts in PLANS:  # one model per plan (the plan is part of the model's configuration)
+        torch.manual_seed(0)
+        m = TinyGPT(68, 1024, n_layer=12, n_head=8, n_embd=512, dropout=0.1, label_smoothing=0.05,
+                    compute_dtype="bf16", device=dev, engine_opts=opts)
+        m.train()
+        models[name] = (m, FusedAdamW(m, lr=3e-4, weight_decay=0.05))
     rng = np.random.default_rng(0)
     tok = torch.from_numpy(rng.integers(4, 68, size=(16, 1025))).to(dev)
     x, y = tok[:, :-1].contiguous(), tok[:, 1:].contiguous()
     side = torch.cuda.Stream(dev)
     main_s = torch.cuda.current_stream(dev)
-    nbytes = {k: 4 * (e - b) for k, (b, e) in bucket_ranges(m).items()}
+    nbytes = {k: 4 * (e - b) for k, (b, e) in bucket_ranges(models["5/5/2"][0]).items()}
 
-    def step(nch, busbw):
+    def step(m, opt, nch, busbw):
         opt.zero_grad(set_to_none=True)
         _, loss = m(x, y)
         if nch:
@@ -65,27 +69,23 @@ def main():
             main_s.wait_event(ev)
         opt.step()
 
-    cases = [(p, nch, bw) for p in PLANS for nch, bw in [(0, 0.0)] + [(n, b) for n in (8, 16) for b in busbws]]
+    cases = [(p, nch, bw) for p, _ in PLANS for nch, bw in [(0, 0.0)] + [(n, b) for n in (8, 16) for b in busbws]]
     times = {c: [] for c in cases}
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(4):
         for plan, nch, bw in cases:
-            _, order, grp = plan
-            L.lib.cg_set_dw_order(order)
-            L.lib.cg_set_dw_group(grp)
-            step(nch, bw)  # warm (re-plans the groups, re-sizes the workspace)
+            m, opt = models[plan]
+            step(m, opt, nch, bw)  # warm
             torch.cuda.synchronize()
             s.record()
             for _ in range(5):
-                step(nch, bw)
+                step(m, opt, nch, bw)
             e.record()
             e.synchronize()
             times[(plan, nch, bw)].append(s.elapsed_time(e) / 5)
-    L.lib.cg_set_dw_order(1)
-    L.lib.cg_set_dw_group(0)
     for (plan, nch, bw), t in times.items():
         tag = "no comm" if not nch else f"{nch:2d} CUs, busbw {bw:4.0f} GB/s"
-        print(f"plan {plan[0]:6s} {tag:28s} step {min(t):6.3f} ms (median {statistics.median(t):6.3f})", flush=True)
+        print(f"plan {plan:6s} {tag:28s} step {min(t):6.3f} ms (median {statistics.median(t):6.3f})", flush=True)
 
 
 if __name__ == "__main__":

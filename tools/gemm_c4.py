@@ -97,14 +97,15 @@ def main():
     torch.cuda.synchronize()
     only = sys.argv[1] if len(sys.argv) > 1 and sys.argv[1] else None  # e.g. "fc2 dX": time only matching rows
     rows = [r for r in rows if only is None or r[0].startswith(only)]
-    # GEMM_VARIANTS="base,pp1,pp2,pp1+pp2": the persistent-tile variants to interleave
-    # (base: neither ping-pong kernel; ppN: cg_gemm_set_pers_pp(N); pp2: cg_gemm_set_pers_pp2(1))
+    # GEMM_VARIANTS="auto,pers,lw": the persistent-tile kernels to interleave (cg_gemm_desc.tile:
+    # automatic, the eight-wave kernel, the loader-wave kernel)
+    import functools
     import os
+    gemm0 = ops.gemm
 
     def set_variant(v):
-        parts = v.split("+")
-        L.lib.cg_gemm_set_pers_pp(next((int(t[2:]) for t in parts if t.startswith("pp") and t != "pp2"), 0))
-        L.lib.cg_gemm_set_pers_pp2(1 if "pp2" in parts else 0)
+        ops.gemm = functools.partial(gemm0, tile={"auto": L.TILE_AUTO, "pers": L.TILE_PERS,
+                                                  "lw": L.TILE_PERS_LW}[v])
 
     modes = [v for v in os.environ.get("GEMM_VARIANTS", "").split(",") if v] or [None]
     bests = {m: {} for m in modes}

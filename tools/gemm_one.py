@@ -1,8 +1,8 @@
-"""One C4 persistent-GEMM product, a few launches per variant, for rocprofv3 --pmc passes.
+"""One C4 persistent-GEMM product, a few launches per kernel, for rocprofv3 --pmc passes.
 
     GEMM_ONE="fc1f" python tools/gemm_one.py     (fc1f: fc1 forward plain, fc1dx: fc1 dX plain)
-Variants run in order: base (loader-wave kernel), pp1 (gemm_pp.h), pp2 (gemm_pp2.h); each kernel
-name in the counter CSV tells them apart.
+Kernels run in order: the eight-wave persistent kernel (CG_TILE_PERS), the loader-wave one
+(CG_TILE_PERS_LW); each kernel name in the counter CSV tells them apart.
 """
 import os
 import sys
@@ -18,10 +18,8 @@ g = torch.Generator().manual_seed(0)
 a = torch.randn(M, K, generator=g).to("cuda", torch.bfloat16)
 b = (torch.randn(N, K, generator=g) * K ** -0.5).to("cuda", torch.bfloat16)
 o = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
-for pp, pp2 in ((0, 0), (1, 0), (0, 1)):
-    L.lib.cg_gemm_set_pers_pp(pp)
-    L.lib.cg_gemm_set_pers_pp2(pp2)
+for tile in (L.TILE_PERS, L.TILE_PERS_LW):
     for _ in range(3):
-        ops.gemm(a, b, out=o)
+        ops.gemm(a, b, out=o, tile=tile)
 torch.cuda.synchronize()
 print("ok")
