@@ -322,7 +322,9 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
       load_row(row, cur);
     }
     RowIn nxt;
-    if constexpr (PF) load_row(min(row + 4, r_end - 1), nxt);  // the last row's reload is unused
+    if constexpr (PF) {
+      if (row + 4 < r_end) load_row(row + 4, nxt);  // wave-uniform: rows past r_end belong to no wave here
+    }
     const float mu = cur.mu, rs = cur.rs;
     const float* gi = g_in ? g_in + (long long)row * cols : nullptr;
     float xh[NV][W], gy[NV][W];

@@ -43,7 +43,7 @@ def dw_block_bytes(c):
     hd = d // c["n_head"]
     kvd = (c["kv"] or c["n_head"]) * hd
     nqkv = d + 2 * kvd
-    M = c["batch"] * c["block_size"]
+    M = c["micro_batch"] * c["block_size"]
     if c["swiglu"]:
         hp = -(-int(8 * d // 3) // 64) * 64
         prods = [(d, hp), (2 * hp, d), (d, d), (nqkv, d)]
@@ -63,7 +63,9 @@ def main():
     out = []
     for (_, name, fb), (_, _, wb) in zip(fetch, write):
         out.append({"kernel": name, "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": 2 * fb + wb})
+    bj = json.loads(Path(bench_json).read_text()) if bench_json else None
     res = {"probe": probe, "kernel": sorted({o["kernel"] for o in out}), "config": cfg, "commit": commit,
+           "micro_batch": bj["config"]["micro_batch_per_gpu"] if bj else c["batch"],
            "launches_counted": len(out),
            "hbm_bytes_per_launch": round(sum(o["hbm_bytes"] for o in out) / len(out)),
            "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate runs of `python "
@@ -71,14 +73,14 @@ def main():
                      "FETCH_SIZE (gfx950 counts wide streaming reads at half) + WRITE_SIZE, KB units, averaged over "
                      "every launch of the class"}
     if probe == "gemm_dw_grouped":
-        per_block, dw_block = dw_block_bytes(c)
+        per_block, dw_block = dw_block_bytes(dict(c, micro_batch=res["micro_batch"]))
         for o in out:
             o["blocks"] = max(1, round(o["write_bytes"] / dw_block))
             o["algorithmic_bytes"] = o["blocks"] * per_block
         res["algorithmic_bytes_per_launch"] = round(sum(o["algorithmic_bytes"] for o in out) / len(out))
         res["algorithmic_source"] = "dY and X operands (bf16) once + dW (fp32) once per block in the group"
     else:
-        b = json.loads(Path(bench_json).read_text())
+        b = bj
         assert b["roofline"]["kernel"] == probe, b["roofline"]["kernel"]
         res["algorithmic_bytes_per_launch"] = b["roofline"]["algorithmic_bytes_per_launch"]
         res["algorithmic_source"] = f"{bench_json}: roofline.algorithmic_bytes_per_launch (library probe)"
