@@ -13,7 +13,8 @@ import torch  # noqa: E402
 from codonlm_amd import _lib as L, ops  # noqa: E402
 
 dev = "cuda"
-M, D = 16384, 512
+import os  # noqa: E402
+M, D = int(os.environ.get("GEMM_M", 16384)), 512  # GEMM_M=32768: the B=32 bench step
 
 
 def timer(fn, it=10):
@@ -100,7 +101,6 @@ def main():
     # GEMM_VARIANTS="auto,pers,lw": the persistent-tile kernels to interleave (cg_gemm_desc.tile:
     # automatic, the eight-wave kernel, the loader-wave kernel)
     import functools
-    import os
     gemm0 = ops.gemm
 
     def set_variant(v):
