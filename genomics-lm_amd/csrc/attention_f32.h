@@ -246,7 +246,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_f32mfma(const float* __restri
 }
 
 static inline bool attn_f32mfma_supported(int hd, const void* qkv, long long ld, const void* y, long long ldy) {
-  if (getenv("CG_ATTN_VEC")) return false;  // diagnostic: force the vector kernels
   return hd > 0 && hd <= 64 && hd % 8 == 0 && ld % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)qkv & 15) == 0 &&
          ((uintptr_t)y & 15) == 0;
 }

@@ -1137,7 +1137,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 
 // ----------------------------------------------------------------------------
 static inline bool attn_mfma_supported(int hd, long long ld_in, long long ld_out) {
-  if (getenv("CG_ATTN_VEC")) return false;  // diagnostic: force the vector kernels
   return (hd == 32 || hd == 48 || hd == 64) && (ld_in % 8 == 0) && (ld_out % 8 == 0);
 }
 

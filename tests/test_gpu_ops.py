@@ -916,28 +916,33 @@ def test_gemm_rope_epilogue_unsupported():
 @pytest.mark.parametrize("B,T,H,KV,hd,window,p", [(2, 1024, 8, 8, 64, 0, 0.1), (2, 512, 8, 4, 48, 0, 0.0),
                                                    (2, 300, 4, 2, 32, 0, 0.1), (1, 257, 4, 1, 24, 37, 0.2),
                                                    (2, 130, 2, 2, 8, 0, 0.0)])
-def test_attention_bwd_f32mfma_vs_vector(B, T, H, KV, hd, window, p, monkeypatch):
+def test_attention_bwd_f32mfma_vs_fp64(B, T, H, KV, hd, window, p):
     """The fp32 attention backward on v_mfma_f32_32x32x2_f32 (attention_f32.h; the reference's own
-    fp32 GPU training, loop.py:498) against the fp32 vector kernels it replaced (CG_ATTN_VEC=1) on
-    the same forward: both are fp32 FMA chains in different orders, so dQ / dK / dV agree to
-    rel <= 2e-5 of each block's scale.  Covers C4 / C3 geometry, GQA, a local window, odd head
-    dims (24, 8), ragged T and dropout keep bits."""
+    fp32 GPU training, loop.py:498; the vector kernels where the head dim is not 32 / 48 / 64)
+    against fp64 autograd of the same masked, dropped-out attention (the oracle's mask and keep
+    bits): dQ / dK / dV agree to rel <= 2e-5 of each block's scale.  Covers C4 / C3 geometry, GQA,
+    a local window, odd head dims (24, 8), ragged T and dropout keep bits."""
     ops = _ops()
     g = torch.Generator().manual_seed(T * 7 + hd)
     N = (H + 2 * KV) * hd
-    qkv = torch.randn(B * T, N, generator=g).to(DEV)
+    qkv = torch.randn(B * T, N, generator=g)
     idx = torch.randint(4, 68, (B, T), generator=g)
     idx[0, T // 3] = 3
     idx[-1, T // 2] = 3
+    drop = None
+    if p > 0:
+        keep = O.dropout_keep(31, np.arange(B * H * T)[:, None], np.arange(T)[None, :], p)
+        drop = torch.from_numpy(keep.astype(np.float64) / (1 - p)).view(B, H, T, T)
     seg = ops.segment_starts(idx.to(DEV), 3)
-    y, lse = ops.attn_fwd(qkv, seg, B, T, H, KV, hd, window=window, drop_seed=31, drop_p=p)
-    dy = torch.randn(B * T, H * hd, generator=g).to(DEV)
-    got = ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, KV, hd, window=window, drop_seed=31, drop_p=p)
-    monkeypatch.setenv("CG_ATTN_VEC", "1")
-    ref = ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, KV, hd, window=window, drop_seed=31, drop_p=p)
-    monkeypatch.delenv("CG_ATTN_VEC")
+    qd = qkv.to(DEV)
+    y, lse = ops.attn_fwd(qd, seg, B, T, H, KV, hd, window=window, drop_seed=31, drop_p=p)
+    dy = torch.randn(B * T, H * hd, generator=g)
+    got = ops.attn_bwd(qd, seg, y, dy.to(DEV), lse, B, T, H, KV, hd, window=window, drop_seed=31, drop_p=p).cpu()
+    qr = qkv.double().requires_grad_(True)
+    _attn_ref(qr, idx, B, T, H, KV, hd, 3, window or None, drop).backward(dy.double())
+    ref = qr.grad
     for name, sl in (("dq", slice(0, H * hd)), ("dk", slice(H * hd, (H + KV) * hd)),
                      ("dv", slice((H + KV) * hd, N))):
-        a, r = got[:, sl].double(), ref[:, sl].double()
+        a, r = got[:, sl].double(), ref[:, sl]
         err = float((a - r).abs().max() / r.abs().max())
         assert err <= 2e-5, (name, err)
