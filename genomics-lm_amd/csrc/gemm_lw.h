@@ -396,7 +396,7 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
             for (int j = 0; j < 8; ++j) s[j] = v[j];
           }
           if constexpr (CT == CG_BF16) {
-            bst(rx, o, pack_bf16(s));
+            bst_aux(rx, o, pack_bf16(s));
           } else {
             bst(rx, o, (u32x4){__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])});
             bst(rx, o + 16, (u32x4){__float_as_uint(s[4]), __float_as_uint(s[5]), __float_as_uint(s[6]), __float_as_uint(s[7])});

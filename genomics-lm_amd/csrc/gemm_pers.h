@@ -77,6 +77,13 @@ __device__ __forceinline__ u32x4 bld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
+// the GELU-derivative / pre-activation store: read again only by the backward, after the rest of
+// the forward has streamed through L2 and the Infinity Cache, so it is written nontemporal
+// (cache-policy bit nt = 2 on gfx950).  Round 5, same-box A/B of the C4 step: default policy
+// 15.13 ms, nt 14.92 ms, sc0 sc1 15.23 ms (profiles/round5/nt_stores_ab.txt).
+__device__ __forceinline__ void bst_aux(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 2);
+}
 __device__ __forceinline__ void unpack_f32(u32x4 a, u32x4 b, float v[8]) {
   v[0] = __uint_as_float(a.x); v[1] = __uint_as_float(a.y); v[2] = __uint_as_float(a.z); v[3] = __uint_as_float(a.w);
   v[4] = __uint_as_float(b.x); v[5] = __uint_as_float(b.y); v[6] = __uint_as_float(b.z); v[7] = __uint_as_float(b.w);
@@ -481,7 +488,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_pers_kernel(GemmParams p) {
             for (int j = 0; j < 8; ++j) s[j] = v[j];
           }
           if constexpr (CT == CG_BF16) {
-            bst(rx, o, pack_bf16(s));
+            bst_aux(rx, o, pack_bf16(s));
           } else {
             bst(rx, o, (u32x4){__float_as_uint(s[0]), __float_as_uint(s[1]), __float_as_uint(s[2]), __float_as_uint(s[3])});
             bst(rx, o + 16, (u32x4){__float_as_uint(s[4]), __float_as_uint(s[5]), __float_as_uint(s[6]), __float_as_uint(s[7])});
