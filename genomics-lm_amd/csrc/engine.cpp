@@ -99,7 +99,13 @@ static int dw_tile_for(const Dims& D, int n, double* cost_out, int* ks_out, long
     for (int ks = 1; ks <= 3; ++ks) {
       if (D.force_ks && ks != D.force_ks) continue;
       const double slab = (double)(ks - 1) * n * dw_block_elems(D) * 20.0 / 5e12 / (11e-9 * (double)M);
-      const double cost = (double)((n * per_layer * ks + cus - 1) / cus) * tile_cost / ks + slab;
+      // the 256 x 128 tile split in two token ranges over several rounds runs 1.35x slower per
+      // item than the model's k-loop share: C4 at B = 32, a 4-block group's 768 items took 1003 us
+      // against the modelled 796; pricing it so moves that plan from 8/4 to 5/5/2, 14.81 -> 14.64
+      // ms/step, with C2 / C3 / C5 on their unchanged plans (profiles/round5/dw_plan_b32.txt)
+      const int rounds = (n * per_layer * ks + cus - 1) / cus;
+      const double split_pen = (bm == 256 && ks == 2 && rounds >= 2) ? 1.35 : 1.0;
+      const double cost = (double)rounds * tile_cost / ks * split_pen + slab;
       if (cost < best_cost - 1e-9) best_cost = cost, best = bm, best_ks = ks;
     }
   }

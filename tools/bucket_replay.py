@@ -11,12 +11,12 @@ bucket's modelled ring time over xGMI,
     t = 2 (n - 1) / n * bytes / busbw,   n = 8 GPUs,
 
 and the step time (fwd + bwd + the side stream + AdamW, synchronised) is measured for each dW
-group plan -- 2/5/5 (short group first), 5/5/2 (short group last, the default since round 4),
-4/4/4, 6/6 --
+group plan -- the planner's own choice, 5/5/2, 4/4/4, 3/3/3/3, 6/6 (remainder group last) --
 and each (NCH, busbw) pair.  Interleaved rounds, min and median.
 
-    python tools/bucket_replay.py [busbw_GBs ...]
+    BR_B=32 python tools/bucket_replay.py [busbw_GBs ...]     (BR_B: sequences per GPU, default 32)
 """
+import os
 import statistics
 import sys
 from pathlib import Path
@@ -30,8 +30,9 @@ from codonlm_amd.optim import FusedAdamW  # noqa: E402
 from codonlm_amd.training.ddp import bucket_ranges  # noqa: E402
 
 # (name, engine_opts): the dW group plans (cg_model_opts dw_remainder_first / dw_group)
-PLANS = [("2/5/5", {"dw_remainder_first": 1}), ("5/5/2", {}), ("4/4/4", {"dw_remainder_first": 1, "dw_group": 4}),
-         ("6/6", {"dw_remainder_first": 1, "dw_group": 6})]
+PLANS = [("planner", {}), ("5/5/2", {"dw_group": 5}), ("4/4/4", {"dw_group": 4}), ("3/3/3/3", {"dw_group": 3}),
+         ("6/6", {"dw_group": 6})]
+B = int(os.environ.get("BR_B", "32"))
 
 
 def main():
@@ -45,11 +46,16 @@ def main():
         m.train()
         models[name] = (m, FusedAdamW(m, lr=3e-4, weight_decay=0.05))
     rng = np.random.default_rng(0)
-    tok = torch.from_numpy(rng.integers(4, 68, size=(16, 1025))).to(dev)
+    tok = torch.from_numpy(rng.integers(4, 68, size=(B, 1025))).to(dev)
+    G, tm, ks = L.C.c_int(0), L.C.c_int(0), L.C.c_int(0)
+    for name, (m, _) in models.items():
+        L.check(L.lib.cg_model_dw_plan(L.C.byref(m.engine.model.cfg), B, 1024, L.C.byref(G), L.C.byref(tm),
+                                       L.C.byref(ks)), "cg_model_dw_plan")
+        print(f"plan {name}: groups of {G.value} blocks, tile {tm.value}, token split {ks.value}", flush=True)
     x, y = tok[:, :-1].contiguous(), tok[:, 1:].contiguous()
     side = torch.cuda.Stream(dev)
     main_s = torch.cuda.current_stream(dev)
-    nbytes = {k: 4 * (e - b) for k, (b, e) in bucket_ranges(models["5/5/2"][0]).items()}
+    nbytes = {k: 4 * (e - b) for k, (b, e) in bucket_ranges(models["planner"][0]).items()}
 
     def step(m, opt, nch, busbw):
         opt.zero_grad(set_to_none=True)
