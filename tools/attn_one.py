@@ -8,7 +8,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "genomics-lm_amd
 import torch
 from codonlm_amd import ops
 
-B, H, T, hd = 16, 8, 1024, 64
+B, H, T, hd = int(os.environ.get("ATTN_B", "32")), 8, 1024, 64  # ATTN_B: the bench's B (32 since round 5)
 g = torch.Generator().manual_seed(0)
 qkv = (torch.randn(B * T, 3 * H * hd, generator=g) * 0.5).to("cuda", torch.bfloat16)
 idx = torch.randint(4, 68, (B, T), generator=g)
