@@ -537,9 +537,10 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       pb = keep_b(pb, 1, w);
     }
     if constexpr (DROP == 3) {
-      // the lane's 8 key pairs (pair r/2 of r = 0, 2, .., 14: colpair k0/2 + 16 kb + 2 hl +
-      // (r&3)/2 + 4 (r>>2)) hashed as attn_drop_mask_kernel does and shifted in, highest first, so
-      // pair r/2 lands on bit r/2 (even key) / 16 + r/2 (odd key)
+      // the lane's 8 key pairs (pair i = r/2 of r = 0, 2, .., 14: colpair k0/2 + 16 kb + 2 hl +
+      // (r&3)/2 + 4 (r>>2)) hashed as attn_drop_mask_kernel does and shifted in, highest first, by
+      // 1 or 3 places, so pair i lands directly on its memory ("pair-split") position kbit(2i) =
+      // {0,1,4,5,8,9,12,13}[i] (even key) / 16 + kbit(2i) (odd key): no reshuffle afterwards
       const uint32_t hb = hrow + ((uint32_t)(k0 >> 1) + 2u * (uint32_t)hl + 16u * (uint32_t)kb) * CG_COLK;
       v4u_a va = __builtin_bit_cast(v4u_a, pa), vb = __builtin_bit_cast(v4u_a, pb);
       uint32_t wl = 0;
@@ -547,20 +548,25 @@ __global__ __launch_bounds__(256, ATTN_FWD_WPS) void attn_fwd_mfma(const bf16_t*
       for (int r = 14; r >= 0; r -= 2) {
         const uint32_t h = cg_pair_mix(hb + (uint32_t)(((r & 3) >> 1) + 4 * (r >> 2)) * CG_COLK);
         // both halves at once: keep = 1 where half >= thr (clamped h - (thr - 1) > 0), shifted into
-        // wl, and the packed pair's 16-bit lanes and-ed with 0 - keep
+        // wl, and the packed bf16 pair's 16-bit lanes multiplied by keep (x 1 keeps the bits, x 0
+        // is +0: one v_pk_mul_lo_u16 where a mask would take a negate and an and)
         uint32_t kp;
-        asm("v_pk_sub_u16 %0, %2, %3 clamp\n\tv_pk_min_u16 %0, %0, 1 op_sel_hi:[1,0]\n\t"
-            "v_lshl_or_b32 %1, %1, 1, %0\n\tv_pk_sub_u16 %0, 0, %0"
-            : "=&v"(kp), "+v"(wl) : "v"(h), "s"(thr2m1));
-        if (r < 8) va[r >> 1] &= kp;
-        else vb[(r - 8) >> 1] &= kp;
+        asm("v_pk_sub_u16 %0, %1, %2 clamp\n\tv_pk_min_u16 %0, %0, 1 op_sel_hi:[1,0]"
+            : "=&v"(kp) : "v"(h), "s"(thr2m1));
+        // the shift applied when pair i goes in moves pairs i+1.. up: 1 for even i, 3 for odd i
+        if ((r >> 1) & 1) asm("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(wl) : "v"(kp));
+        else asm("v_lshl_or_b32 %0, %0, 1, %1" : "+v"(wl) : "v"(kp));
+        // (a compiler-visible packed multiply: the PV MFMA reads this register next, and hipcc
+        // inserts the VALU-write -> MFMA-read wait states only after its own instructions)
+        typedef unsigned short u16x2_k __attribute__((ext_vector_type(2)));
+        const uint32_t pr = r < 8 ? va[r >> 1] : vb[(r - 8) >> 1];
+        const uint32_t pm = __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2_k, pr) * __builtin_bit_cast(u16x2_k, kp));
+        if (r < 8) va[r >> 1] = pm;
+        else vb[(r - 8) >> 1] = pm;
       }
       pa = __builtin_bit_cast(v8bf, va);
       pb = __builtin_bit_cast(v8bf, vb);
-      // memory ("pair-split") order: bit i of each half -> kbit(2i) = {0,1,4,5,8,9,12,13}[i], + 2 hl
-      const uint32_t sp = (wl & 0x00030003u) | ((wl & 0x000C000Cu) << 2) | ((wl & 0x00300030u) << 4) |
-                          ((wl & 0x00C000C0u) << 6);
-      wout = sp << (2 * hl);
+      wout = wl << (2 * hl);  // (+ 2 hl: the lane half's keys)
     }
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 0, 0), pa, o0, 0, 0, 0);
     o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Vi, to, 32 * kb, 1, 0), pb, o0, 0, 0, 0);
