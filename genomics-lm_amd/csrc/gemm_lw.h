@@ -285,8 +285,8 @@ __global__ __launch_bounds__(bfl::THREADS, 1) void gemm_bf16_lw_kernel(GemmParam
           }
         const bool ok = off_c[i][0] != OOR;
         const uint32_t o = ok ? (uint32_t)(((long long)row * p.ld_aux + col[0]) * 2) : OOR;
-        bst(rx, o, pack_bf16(g));
-        bst(rx, ok ? o + (uint32_t)p.N * 2u : OOR, pack_bf16(u));
+        bst_aux(rx, o, pack_bf16(g));  // (read again only by the backward: nontemporal)
+        bst_aux(rx, ok ? o + (uint32_t)p.N * 2u : OOR, pack_bf16(u));
 #pragma unroll
         for (int j = 0; j < 8; ++j) sv[j] = col[0] + j < p.n_valid ? silu_f(g[j]) * u[j] : 0.f;
         bst(rc, off_c[i][0], pack_bf16(sv));
