@@ -187,6 +187,12 @@ __device__ __forceinline__ float keep_f(float v, uint32_t w, int bit) {
   asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(m) : "v"(w), "i"(bit));
   return __int_as_float(__float_as_int(v) & m);
 }
+// (m & a) | (~m & b) as one gfx950 v_bitop3_b32 (truth table 0xCA; hipcc lowers the plain select
+// to and / xor chains here).  A builtin, not inline asm: `a` is an MFMA accumulator, and hipcc pads
+// the XDL-write -> VALU-read hazard only before instructions it generates itself
+__device__ __forceinline__ float bsel(uint32_t m, float a, float b) {
+  return __uint_as_float(__builtin_amdgcn_bitop3_b32(m, __float_as_uint(a), __float_as_uint(b), 0xCA));
+}
 // all-ones / zero from constant bit `bit` of w
 __device__ __forceinline__ int keep_mask_i(uint32_t w, int bit) {
   int m;
@@ -797,8 +803,8 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
             s[r + 1] = p1 * ((hsh >> 16) >= thr ? dp[r + 1] : nd);
           } else if constexpr (DROP == 2) {
             const uint32_t m0 = (uint32_t)keep_mask_i(wb, kbit(r)), m1 = (uint32_t)keep_mask_i(wb, kbit(r + 1));
-            s[r] = p0 * __uint_as_float((__float_as_uint(dp[r]) & m0) | (__float_as_uint(nd) & ~m0));
-            s[r + 1] = p1 * __uint_as_float((__float_as_uint(dp[r + 1]) & m1) | (__float_as_uint(nd) & ~m1));
+            s[r] = p0 * bsel(m0, dp[r], nd);
+            s[r + 1] = p1 * bsel(m1, dp[r + 1], nd);
           } else {
             s[r] = p0 * dp[r];
             s[r + 1] = p1 * dp[r + 1];
@@ -1060,7 +1066,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
           } else if constexpr (DROP == 2) {
             const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
             pdr = __uint_as_float(__float_as_uint(p) & m);
-            s[r] = p * __uint_as_float((__float_as_uint(dp[r]) & m) | (__float_as_uint(nd[r]) & ~m));
+            s[r] = p * bsel(m, dp[r], nd[r]);
           } else {
             s[r] = p * dp[r];
           }
