@@ -84,6 +84,19 @@ __device__ __forceinline__ void stw(float* p, const float* v) {
   if constexpr (W == 4) *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
   else *(float2*)p = make_float2(v[0], v[1]);
 }
+// the residual-gradient row: read again only by the next LayerNorm backward, several kernels
+// later, so it is stored nontemporal (round 5, same-box A/B of the C4 step: 14.57 -> 14.50 ms,
+// profiles/round5/nt_stores_ab.txt)
+template <int W>
+__device__ __forceinline__ void stw_g(float* p, const float* v) {
+  if constexpr (W == 4) {
+    typedef float f4_nt __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store((f4_nt){v[0], v[1], v[2], v[3]}, (f4_nt*)p);
+  } else {
+    typedef float f2_nt __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store((f2_nt){v[0], v[1]}, (f2_nt*)p);
+  }
+}
 template <int W>
 __device__ __forceinline__ void stw(bf16_t* p, const float* v) {
   uint32_t u[W / 2];
@@ -356,7 +369,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec(const TD* __restrict__ dy, lon
 #pragma unroll
         for (int j = 0; j < W; ++j) o[j] += g2[i][j];
       }
-      stw<W>(go + c, o);
+      stw_g<W>(go + c, o);
       if (g_out_t) {
         if (thr) {
 #pragma unroll
