@@ -68,3 +68,60 @@ def test_c4_bench_batch_rows_match_small_batch(c4_bench):
             e = _rel_l2(part, full[r:r + 2])
             print(f"[C4 rows {r}-{r + 1}] B=2 vs B={B_BENCH}: max |dlogit| {d:.3e}, rel-L2 {e:.2e}")
             assert e <= LOGIT_REL_L2_BF16 / 5, (r, e)
+
+
+# the other configs' bench batches (bench.py CONFIGS): the reference's sequences per optimizer step
+def _bench_batch(name):
+    from bench import CONFIGS as BC
+    return BC[name.lower()]["batch"]
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C5"])
+def test_bench_batch_consistency(name):
+    """C2 / C3 / C5 at their bench batch (the B=2 oracle parity of test_gpu_configs plans the dW
+    groups for the same token count; here the kernels run the full geometry): the bf16 step's
+    logits rows equal B=2 runs of the same rows (bf16-level), and its parameter gradients equal the
+    loss-weight-weighted sum of four quarter-batch steps (each with its own, different dW plan) --
+    the LM loss is a weighted mean over valid targets, so grad(B) = sum_i (W_i / W) grad(B_i)."""
+    cfg, _ = _cfg(name)
+    params = O.synthetic_params(cfg, seed=17 + len(name))
+    B, T = _bench_batch(name), cfg.block_size
+    x, y = packed_batch(B, T, seed=9)
+    m = _model(cfg, params, "bf16")
+    xd, yd = torch.from_numpy(x).to(DEV), torch.from_numpy(y).to(DEV)
+    w = torch.tensor(cfg.loss_weights if cfg.loss_weights else [1.0] * cfg.vocab_size, dtype=torch.float64)
+
+    def wsum(yy):
+        yy = torch.from_numpy(yy)
+        return float(torch.where(yy != 0, w[yy], torch.zeros(()).double()).sum())
+
+    m.zero_grad(set_to_none=True)
+    logits, loss = m(xd, yd)
+    loss.backward()
+    torch.cuda.synchronize()
+    full = {k: p.grad.detach().double().cpu().clone() for k, p in m.named_parameters() if p.grad is not None}
+    lg = logits.detach().float().cpu().reshape(B, T, -1)
+    acc = {k: torch.zeros_like(v) for k, v in full.items()}
+    W = wsum(y)
+    q = B // 4
+    for i in range(4):
+        sl = slice(i * q, (i + 1) * q)
+        m.zero_grad(set_to_none=True)
+        li, lossi = m(xd[sl].contiguous(), yd[sl].contiguous())
+        lossi.backward()
+        torch.cuda.synchronize()
+        if i in (0, 3):
+            part = li.detach().float().cpu().reshape(q, T, -1)
+            e = _rel_l2(part, lg[sl])
+            print(f"[{name} B={B}] logits rows {sl.start}-{sl.stop - 1} vs quarter run: rel-L2 {e:.2e}")
+            assert e <= LOGIT_REL_L2_BF16 / 5, (name, i, e)
+        wi = wsum(y[sl]) / W
+        for k, p in m.named_parameters():
+            if k in acc and p.grad is not None:
+                acc[k] += wi * p.grad.detach().double().cpu()
+    # (without RoPE the key biases' gradients are zero in exact arithmetic -- softmax shift
+    # invariance -- so both sides are rounding noise and are left out, as in _check_bf16)
+    worst = sorted(((_rel_l2(acc[k], v), k) for k, v in full.items()
+                    if float(v.norm()) > 0 and not (k.endswith("attn.key.bias") and not cfg.use_rope)), reverse=True)
+    print(f"[{name} B={B}] gradient vs weighted quarter sum: worst {[(k, f'{e:.2e}') for e, k in worst[:3]]}")
+    assert worst[0][0] <= 1e-2, (name, worst[:3])
