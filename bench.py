@@ -41,11 +41,15 @@ import torch.distributed as dist  # noqa: E402
 CONFIGS = {
     # BASELINE.json configs[3] (the metric's config); the others are the remaining GPU configs
     "c4": dict(n_layer=12, n_head=8, n_embd=512, block_size=1024, batch=32, swiglu=False, rope=False, kv=None),
-    "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, batch=64, swiglu=False, rope=False, kv=None),
-    "c3": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=64, swiglu=True, rope=True, kv=4),
+    # per-GPU microbatch of every config = the sequences of one optimizer step of the reference's
+    # own config for that shape (batch_size x grad_accum_steps): C4 2 x 16 (runs/2025-11-05_tiny_
+    # 12L8H_d512_e5/log.txt:30-31), C2 4 x 64 (configs/stage2.5_master.yaml:25-26), C3 8 x 32
+    # (configs/bench_b8_gqa4.yaml:1,6), C5 4 x 32 (configs/stage2.6_large_scaling.yaml:25-26)
+    "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, batch=256, swiglu=False, rope=False, kv=None),
+    "c3": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=256, swiglu=True, rope=True, kv=4),
     # stage2.6_large_scaling + termination head + multi-offset heads: the trainer's
     # full objective (loop.py:1075-1112) on packed BOS..EOS,SEP segments
-    "c5": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=32, swiglu=False, rope=False, kv=None,
+    "c5": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, batch=128, swiglu=False, rope=False, kv=None,
                offsets=(2, 4, 8, 16, 32), term=True),
 }
 # CPU-baseline batch per BASELINE.md §3 (the reference's default per-device batch)

@@ -46,7 +46,7 @@ GRAD_REL_L2_BF16 = 1.5e-2
 TOL_FP32 = 1e-4
 
 # per-GPU microbatch of each config's bench line (bench.py CONFIGS): the dW plan the parity runs take
-BENCH_B = {"C2": 64, "C3": 64, "C4": 32, "C5": 32}
+BENCH_B = {"C2": 256, "C3": 256, "C4": 32, "C5": 128}
 # (oracle config kwargs, microbatch B); C5 = stage2.6_large_scaling + its aux heads
 CONFIGS = {
     "C1": (dict(n_layer=4, n_head=2, n_embd=128, block_size=512), 2),
