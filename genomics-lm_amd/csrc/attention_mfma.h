@@ -1076,17 +1076,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       pb0 = pack_b(pd, 0); pb1 = pack_b(pd, 1);
       sb0 = pack_b(s, 0); sb1 = pack_b(s, 1);
     };
-    auto phase_dkdv = [&](int qb, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
+    // the transposed dO / Q fragments the dV / dK products read: LDS only, so they are issued before
+    // the half's softmax / keep VALU (a scheduling barrier keeps them there) and land under it
+    struct TrFr { v8bf d[4], q[4]; };
+    auto tr_frags = [&](int qb, TrFr& f) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < (hd > 32 ? 4 : 2); ++i) {
+        f.d[i] = frag_tr_o(Di, to, qb * 32, i & 1, i >> 1);
+        f.q[i] = frag_tr_o(Qi, to, qb * 32, i & 1, i >> 1);
+      }
+    };
+    auto phase_dkdv = [&](const TrFr& f, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
                           __attribute__((always_inline)) {
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 0), pb0, dv0, 0, 0, 0);
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 0), pb1, dv0, 0, 0, 0);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 0), sb0, dk0, 0, 0, 0);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 0), sb1, dk0, 0, 0, 0);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[0], pb0, dv0, 0, 0, 0);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[1], pb1, dv0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[0], sb0, dk0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[1], sb1, dk0, 0, 0, 0);
       if constexpr (hd > 32) {
-        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 0, 1), pb0, dv1, 0, 0, 0);
-        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Di, to, qb * 32, 1, 1), pb1, dv1, 0, 0, 0);
-        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 0, 1), sb0, dk1, 0, 0, 0);
-        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Qi, to, qb * 32, 1, 1), sb1, dk1, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[2], pb0, dv1, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[3], pb1, dv1, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[2], sb0, dk1, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[3], sb1, dk1, 0, 0, 0);
       }
     };
     auto body = [&](auto full) __attribute__((always_inline)) {
@@ -1094,9 +1104,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
       for (int qb = 0; qb < 2; ++qb) {
         v16f s, dp, nd;
         v8bf x0, x1, x2, x3;
+        TrFr f;
         phase_sdp(qb, s, dp, nd);
+        tr_frags(qb, f);
+        __builtin_amdgcn_sched_barrier(0);
         phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
-        phase_dkdv(qb, x0, x1, x2, x3);
+        phase_dkdv(f, x0, x1, x2, x3);
       }
     };
     if (active) {
