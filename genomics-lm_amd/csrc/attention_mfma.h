@@ -782,6 +782,11 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
             dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Vi, ro, kb * 32, ks), df[ks], dp, 0, 0, 0);
           }
         }
+        // the dQ product's K^T fragments (LDS only) issued before the softmax / keep VALU below
+        v8bf kt[4];
+#pragma unroll
+        for (int i = 0; i < (hd > 32 ? 4 : 2); ++i) kt[i] = frag_tr_o(Ki, to, kb * 32, i & 1, i >> 1);
+        __builtin_amdgcn_sched_barrier(0);
         const int kq = myq - k0 - kb * 32, kl = lo - k0 - kb * 32;
         if (!full) {
 #pragma unroll
@@ -811,11 +816,11 @@ __global__ __launch_bounds__(256, ATTN_DQ_WPS) void attn_bwd_dq_mfma(const bf16_
           }
         }
         const v8bf b0 = pack_b(s, 0), b1 = pack_b(s, 1);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 0), b0, a0, 0, 0, 0);
-        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 0), b1, a0, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt[0], b0, a0, 0, 0, 0);
+        a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt[1], b1, a0, 0, 0, 0);
         if constexpr (hd > 32) {
-          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 0, 1), b0, a1, 0, 0, 0);
-          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_tr_o(Ki, to, kb * 32, 1, 1), b1, a1, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt[2], b0, a1, 0, 0, 0);
+          a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kt[3], b1, a1, 0, 0, 0);
         }
       }
     };
