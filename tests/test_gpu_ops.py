@@ -845,6 +845,32 @@ def test_gemm_colsum_epilogue(dtype, pers):
     assert (cs.cpu() - base.sum(0)).abs().max() < tol * (1 + base.abs().sum(0).max())
 
 
+@pytest.mark.parametrize("max_wg", [0, 4, 7, 12, 16])
+@pytest.mark.parametrize("tile", ["pers", "lw"])
+def test_gemm_colsum_multi_tile_walk(max_wg, tile):
+    """Column sums carried across a persistent block's tiles (the 8-wave kernel sums consecutive
+    tiles of one column block in registers and writes zero partials for the others): grid caps
+    that divide the 4 column tiles (4, 12, 16: every block walks one column block), that do not
+    (7: the column block changes along the walk) and the full grid, with the dGELU epilogue of
+    the fc2 dX product; M = 2000 leaves a ragged last row tile."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    M, N, K = 2000, 512, 256
+    g = torch.Generator().manual_seed(12)
+    x, w = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.1
+    aux = (torch.rand(M, N, generator=g) * 1.2).to(torch.bfloat16)
+    base = (_bf(x) @ _bf(w).t()) * aux.float()
+    cs = torch.empty(N, device=DEV)
+    t = {"pers": L.TILE_PERS, "lw": L.TILE_PERS_LW}[tile]
+    y = ops.gemm(x.to(DEV, torch.bfloat16), w.to(DEV, torch.bfloat16), out_dtype=torch.bfloat16, colsum_out=cs,
+                 epilogue=L.EPI_DGELU | L.EPI_GELU_DERIV, aux=aux.to(DEV), tile=t, max_wg=max_wg)
+    torch.cuda.synchronize()
+    ref = y.float().cpu().sum(0)  # (the sums are of the fp32 values before the bf16 store)
+    assert (y.float().cpu() - base).abs().max() < 2e-2 * (1 + base.abs().max())
+    assert (cs.cpu() - base.sum(0)).abs().max() < 2e-2 * (1 + base.abs().sum(0).max())
+    assert (cs.cpu() - ref).abs().max() < 1e-2 * (1 + base.abs().sum(0).max())
+
+
 @pytest.mark.parametrize("cap", [1, 3])
 @pytest.mark.parametrize("M,K,T,H,KV,hd,extra", [(16384, 384, 512, 8, 4, 48, 0), (700, 128, 77, 4, 2, 32, 0),
                                                  (513, 256, 513, 2, 1, 64, 64), (300, 128, 100, 1, 1, 48, 0),
