@@ -103,7 +103,7 @@ class TransposeBatch(C.Structure):
 class ModelOpts(C.Structure):
     """cg_model_opts: all zero = the measured defaults"""
     _fields_ = [("dw_group", i32), ("dw_ksplit", i32), ("dw_remainder_first", i32), ("head_dw_separate", i32),
-                ("rope_tables", i32), ("attn_mask_kernel", i32), ("dw_plan_tokens", i32)]
+                ("rope_tables", i32), ("attn_mask_kernel", i32), ("dw_plan_tokens", i32), ("attn_bwd_algo", i32)]
 
 
 class ModelCfg(C.Structure):
@@ -162,6 +162,8 @@ SIGNATURES = {
     "cg_attn_bwd": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
                           u32, f32, vp, vp, i64, vp, sz, vp]),
     "cg_attn_bwd_rope": (i32, [i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
+                               u32, f32, vp, vp, i64, vp, vp, vp, sz, vp]),
+    "cg_attn_bwd_algo": (i32, [i32, i32, vp, i64, vp, vp, i64, vp, i64, vp, vp, i64, i32, i32, i32, i32, i32, i32,
                                u32, f32, vp, vp, i64, vp, vp, vp, sz, vp]),
     "cg_ce_workspace": (sz, [i32]),
     "cg_cross_entropy": (i32, [vp, i64, vp, i32, i32, f32, vp, i32, f32, i32, vp, i64, vp, vp, sz, vp]),

@@ -222,12 +222,16 @@ def attn_fwd_keep(qkv, segstart, B, T, H, KV, hd, drop_seed, drop_p, window=0, m
     return y, lse, mask
 
 
+ATTN_BWD_ALGO = {None: 0, "auto": 0, "split": 1, "fused": 2}
+
+
 def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, drop_p=0.0, drop_mask=None,
-             bias_part=None, rope=None):
+             bias_part=None, rope=None, algo=None):
     """dqkv; with bias_part (fp32 [B*ceil(T/128)][ld >= (H+2KV) hd], bf16 MFMA path) also the per-tile
     column sums of dqkv that cg_colsum_reduce turns into the q/k/v bias gradients.  rope = (cos, sin)
     fp32 [T][hd/2] tables: qkv holds rotated q / k and dQ / dK come back w.r.t. the un-rotated ones
-    (cg_attn_bwd_rope, bf16 MFMA path)."""
+    (cg_attn_bwd_rope, bf16 MFMA path).  algo: None / "auto", "split" (dQ kernel + dK/dV kernel) or
+    "fused" (one pass, cg_attn_bwd_algo) for the bf16 MFMA backward."""
     dqkv = torch.zeros_like(qkv)
     ws = torch.empty(int(L.lib.cg_attn_bwd_workspace(B, T, H)) // 4 + 1, dtype=torch.float32, device=qkv.device)
     args = [_dt(qkv), qkv.data_ptr(), qkv.stride(0), _p(segstart), y.data_ptr(), y.stride(0), dy.data_ptr(),
@@ -235,7 +239,10 @@ def attn_bwd(qkv, segstart, y, dy, lse, B, T, H, KV, hd, window=0, drop_seed=0, 
             int(drop_seed) & 0xFFFFFFFF, float(drop_p), _p(drop_mask), _p(bias_part),
             0 if bias_part is None else bias_part.stride(0)]
     tail = [ws.data_ptr(), ws.numel() * 4, L.stream_ptr(qkv.device)]
-    if rope is None:
+    if algo is not None:
+        rp = [None, None] if rope is None else [rope[0].data_ptr(), rope[1].data_ptr()]
+        L.check(L.lib.cg_attn_bwd_algo(ATTN_BWD_ALGO[algo], *args, *rp, *tail), "cg_attn_bwd_algo")
+    elif rope is None:
         L.check(L.lib.cg_attn_bwd(*args, *tail), "cg_attn_bwd")
     else:
         L.check(L.lib.cg_attn_bwd_rope(*args, rope[0].data_ptr(), rope[1].data_ptr(), *tail), "cg_attn_bwd_rope")

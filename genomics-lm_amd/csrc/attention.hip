@@ -397,27 +397,42 @@ extern "C" int cg_attn_fwd_keep(int dtype, const void* qkv, long long ldqkv, con
                      stream);
 }
 
-// delta (the vector path's rowsum(dO o O); the MFMA path's nd = -delta/dscale) | -lse2 (MFMA path)
-extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) { return 2 * (size_t)B * H * T * sizeof(float); }
+// nd (the vector path's delta = rowsum(dO o O); the MFMA paths' -delta/dscale) | -lse2 (MFMA paths)
+// | dq_acc (the fused pass's fp32 dQ^T sums, attention_mfma.h fa::dqa_off)
+extern "C" size_t cg_attn_bwd_workspace(int B, int T, int H) {
+  return (2 * (size_t)B * H * T + attn_dq_acc_floats(B, T, H)) * sizeof(float);
+}
 
 extern "C" int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const void* y,
                            long long ldy, const void* dy, long long lddy, const float* lse, void* dqkv,
                            long long lddqkv, int B, int T, int H, int KV, int hd, int window, uint32_t drop_seed,
                            float drop_p, const void* drop_mask, float* bias_part, long long ld_part, void* ws,
                            size_t ws_bytes, void* stream) {
-  return cg_attn_bwd_rope(dtype, qkv, ldqkv, segstart, y, ldy, dy, lddy, lse, dqkv, lddqkv, B, T, H, KV, hd, window,
-                          drop_seed, drop_p, drop_mask, bias_part, ld_part, nullptr, nullptr, ws, ws_bytes, stream);
+  return cg_attn_bwd_algo(CG_ATTN_BWD_AUTO, dtype, qkv, ldqkv, segstart, y, ldy, dy, lddy, lse, dqkv, lddqkv, B, T,
+                          H, KV, hd, window, drop_seed, drop_p, drop_mask, bias_part, ld_part, nullptr, nullptr, ws,
+                          ws_bytes, stream);
 }
-// cg_attn_bwd with the gradients of RoPE-rotated q / k rotated back (rope_cos / rope_sin: the
-// [>= T][hd/2] tables of cg_rope_tab; both NULL = no RoPE): the dQ and dK outputs -- and their
-// bias partials -- are w.r.t. the un-rotated q / k projections (the MFMA kernels only; the vector
-// path returns CG_EUNSUPPORTED with tables)
 extern "C" int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
                                 const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
                                 void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
                                 uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
                                 long long ld_part, const float* rope_cos, const float* rope_sin, void* ws,
                                 size_t ws_bytes, void* stream) {
+  return cg_attn_bwd_algo(CG_ATTN_BWD_AUTO, dtype, qkv, ldqkv, segstart, y, ldy, dy, lddy, lse, dqkv, lddqkv, B, T,
+                          H, KV, hd, window, drop_seed, drop_p, drop_mask, bias_part, ld_part, rope_cos, rope_sin, ws,
+                          ws_bytes, stream);
+}
+// cg_attn_bwd with the gradients of RoPE-rotated q / k rotated back (rope_cos / rope_sin: the
+// [>= T][hd/2] tables of cg_rope_tab; both NULL = no RoPE): the dQ and dK outputs -- and their
+// bias partials -- are w.r.t. the un-rotated q / k projections (the MFMA kernels only; the vector
+// path returns CG_EUNSUPPORTED with tables)
+extern "C" int cg_attn_bwd_algo(int algo, int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
+                                const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
+                                void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
+                                uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
+                                long long ld_part, const float* rope_cos, const float* rope_sin, void* ws,
+                                size_t ws_bytes, void* stream) {
+  if (algo < CG_ATTN_BWD_AUTO || algo > CG_ATTN_BWD_FUSED) return CG_EINVAL;
   if (KV <= 0 || H % KV) return CG_EINVAL;
   if ((rope_cos == nullptr) != (rope_sin == nullptr)) return CG_EINVAL;
   if (B > 0 && T > 0 && (!ws || ws_bytes < cg_attn_bwd_workspace(B, T, H))) return CG_EINVAL;
@@ -434,12 +449,14 @@ extern "C" int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, con
   if (rope_cos && (!mfma || hd % 16 || ((uintptr_t)rope_cos & 15) || ((uintptr_t)rope_sin & 15)))
     return CG_EUNSUPPORTED;
   if (mfma) {
-    // delta = rowsum(dO o O) is computed inside the dQ kernel
+    if (algo == CG_ATTN_BWD_FUSED && thr && !drop_mask) return CG_EUNSUPPORTED;  // keep words needed
+    // delta = rowsum(dO o O): inside the split pass's dQ kernel, or the fused pass's pre-pass
     return attn_bwd_mfma_launch((const bf16_t*)qkv, ldqkv, segstart, (const bf16_t*)y, ldy, (const bf16_t*)dy,
                                 lddy, lse, delta, (bf16_t*)dqkv, lddqkv, B, T, H, KV, hd, window, drop_seed, thr,
                                 dscale, scale, (const uint32_t*)drop_mask, bias_part, ld_part, s, rope_cos,
-                                rope_sin);
+                                rope_sin, algo);
   }
+  if (algo == CG_ATTN_BWD_FUSED) return CG_EUNSUPPORTED;
   // fp32: the f32-MFMA kernels (exact fp32 products; delta formed inside the dQ kernel) where the
   // layout allows
   if (dtype != CG_BF16 && attn_f32mfma_supported(hd, qkv, ldqkv, dy, lddy) && (lddqkv & 3) == 0 &&

@@ -141,6 +141,15 @@ __device__ __forceinline__ TrOff tr_offsets(int lane) {
 __device__ __forceinline__ v8bf frag_row_o(const char* img, const RowOff& ro, int rb, int ks) {
   return *(const v8bf*)(img + ro.o[ks] + rb * 128);
 }
+// frag_tr_o with the two half offsets passed explicitly (a runtime column block: indexing TrOff by
+// a runtime cb would put it on the stack)
+__device__ __forceinline__ v8bf frag_tr_p(const char* img, uint32_t o0, uint32_t o1, int rb, int s) {
+  const int d = (rb + 16 * s) * 128;
+  const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + o0 + d));
+  const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + o1 + d));
+  const v8s r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(v8bf, r);
+}
 __device__ __forceinline__ v8bf frag_tr_o(const char* img, const TrOff& to, int rb, int s, int cb) {
   const int d = (rb + 16 * s) * 128;
   const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_p)(img + to.o[cb][0] + d));
@@ -1169,6 +1178,606 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
   }
 }
 
+// ============================================================================
+// fused backward: dK, dV AND dQ in one pass (five MFMA products per tile -- S, dP, dV, dK, dQ --
+// against the two-kernel path's seven; Q, dO, the row statistics and the keep words streamed once).
+// WG = 8 waves x 32 keys = one 256-key block at a time, and the WG owns ONE (b, kv head) for all of
+// its key blocks and query heads.  So the dQ rows of the group's query heads have a single writer:
+// the WG read-modify-writes fp32 dQ^T partials into dq_acc (layout fa::dqa_off), which no other
+// workgroup touches -- no atomics, no cross-workgroup reduction, bitwise reproducible.
+// Per iteration (one 64-query tile of one query head):
+//   * waves 0-3 (one per SIMD) first finish the PREVIOUS tile's dQ^T block -- query half w >> 1,
+//     head-dim block w & 1 -- = K^T[d][256 keys] dS^T[keys][q] (16 MFMAs, operands by
+//     ds_read_b64_tr_b16 from the block's K image and the dS^T image), + the dq_acc value (plain
+//     store on the tile's first visit);
+//   * all waves, as attn_bwd_dkdv_mfma: S and dP (key on the lane, seeded with -lse2 / nd), P and
+//     dS, dV += dO^T P, dK += Q^T dS; the wave's dS^T (bf16, the dK operand itself) goes into the
+//     LDS image dsb[it & 1] ([256 keys][64 queries], dual layout).
+// One barrier per iteration.  Before: attn_bwd_prep_kernel (the -lse2 and nd rows), after:
+// attn_dq_finish_kernel (dq_acc -> the bf16 dqkv q columns, x scale, RoPE inverse, q-bias
+// partials).  Keep bits from the forward's words only (DROP 0 / 2).
+// ============================================================================
+#ifndef FB_DIAG
+#define FB_DIAG 0  // diagnostic builds only (results invalid): 1 phase B without its MFMAs, 2 no phase B
+#endif
+namespace fa {
+constexpr int FB_KEYS = 256;     // keys per block (8 waves x 32)
+constexpr int FB_DSB = 4 * IMG;  // one dS^T image set [256 keys][64 queries] bf16 (also the K image)
+// ring buffer: Q image | dO image | -lse2 | nd | seg | (a slot the row DMAs of waves 3-7 fill) |
+// (DROP 2) the 8 waves' keep words of the tile's 64 queries
+__host__ __device__ constexpr int fb_buf(int drop) { return 2 * IMG + 4 * 64 * 4 + (drop == 2 ? 8 * 64 * 4 : 0); }
+// LDS: 3 ring buffers (first: every per-iteration read is lane offset + a < 64 KiB immediate) | dsb[2] |
+// K image; the first 68 KiB double as the bias column-sum scratch at the end of a key block
+__host__ __device__ constexpr int fb_lds(int drop) { return 3 * FB_DSB + 3 * fb_buf(drop); }
+// dq_acc: [b H + h][query block of 32][64 head dims][32 queries] fp32 -- one accumulator register
+// of a dQ^T block is two 128-B runs (32 queries of one head dim), and its 16 registers sit at
+// constant offsets from the lane's base (immediate-offset loads / stores)
+__host__ __device__ inline long long dqa_off(long long bh, int nq32, int q32, int d) {
+  return ((bh * nq32 + q32) * 64 + d) * 32;
+}
+// one 1-KiB LDS-DMA piece per wave: rows 8 wave .. 8 wave + 7 of a 64-row image (8 waves fill it);
+// the dual_off swizzle on the per-lane source chunk as in tile_dma_src
+struct PieceDma {
+  __amdgpu_buffer_rsrc_t r;
+  uint32_t off;
+};
+__device__ __forceinline__ PieceDma piece_dma_src(const bf16_t* batch_rows, long long ld, int T, int hd, int wave,
+                                                  int lane) {
+  PieceDma p;
+  p.r = __builtin_amdgcn_make_buffer_rsrc((void*)batch_rows, (short)0, (int)((long long)T * ld * 2), 0x00020000);
+  const int row = 8 * wave + (lane >> 3), j = row >> 1;
+  const int ch = (lane & 7) ^ ((j & 7) ^ ((j & 1) << 2));
+  p.off = ch * 8 < hd ? (uint32_t)(((long long)row * ld + ch * 8) * 2) : 0x80000000u;
+  return p;
+}
+__device__ __forceinline__ void piece_dma(uint32_t img, const PieceDma& p, uint32_t ubase, int wave) {
+  dma16(p.r, img + (uint32_t)(8 * wave * 128), p.off + ubase);
+}
+// column sums over the workgroup's 256 accumulator columns (8 waves x 32 lanes) of the 64 rows in
+// x0 / x1 -- colsum_wg for 8 waves; `red` needs COLSUM8_LDS bytes; ends with a barrier
+constexpr int COLSUM8_LDS = (8 * 64 * 33 + 8 * 64) * 4;
+__device__ __forceinline__ float colsum_wg8(const v16f& x0, const v16f& x1, float s, bool ok, float* red, int wave,
+                                            int lane, int tid) {
+  float* t = red + wave * 64 * 33 + (lane & 31);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    t[acc_row(r, lane) * 33] = ok ? x0[r] * s : 0.f;
+    t[(32 + acc_row(r, lane)) * 33] = ok ? x1[r] * s : 0.f;
+  }
+  __syncthreads();
+  const float* run = red + (tid >> 6) * 64 * 33 + (tid & 63) * 33;
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    a += run[k];
+    b += run[k + 1];
+  }
+  float* part = red + 8 * 64 * 33;
+  part[tid] = a + b;
+  __syncthreads();
+  float v = 0.f;
+  if (tid < 64)
+    v = ((part[tid] + part[64 + tid]) + (part[128 + tid] + part[192 + tid])) +
+        ((part[256 + tid] + part[320 + tid]) + (part[384 + tid] + part[448 + tid]));
+  __syncthreads();
+  return v;  // threads 0..63: the column sum of row tid
+}
+// sum over the 32 lanes of each half-wave, in every lane of that half (wave_reduce without its last
+// v_permlane32_swap step)
+__device__ __forceinline__ float half_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  const auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(a[0]) + __uint_as_float(a[1]);
+}
+}  // namespace fa
+
+// nd = -rowsum(dO o O) / dscale (the dP seed; delta of the FA2 preprocessing) and -lse * log2(e)
+// (the S seed), one row per (b, h, query): 8 lanes per row, 16-B loads of dO and O
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __restrict__ dy, long long lddy,
+                                                            const bf16_t* __restrict__ yo, long long ldy,
+                                                            const float* __restrict__ lse, float* __restrict__ nd,
+                                                            float* __restrict__ nlse2, int T, int H, int hd,
+                                                            float inv_dscale, long long nrows) {
+  const long long r = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const int j = threadIdx.x & 7;
+  float s = 0.f;
+  if (r < nrows && 8 * j < hd) {
+    const long long bh = r / T;
+    const int q = (int)(r - bh * T), b = (int)(bh / H), h = (int)(bh - (long long)b * H);
+    const long long row = (long long)b * T + q;
+    const uint4 dv = *(const uint4*)(dy + row * lddy + (long long)h * hd + 8 * j);
+    const uint4 ov = *(const uint4*)(yo + row * ldy + (long long)h * hd + 8 * j);
+    const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, ow[4] = {ov.x, ov.y, ov.z, ov.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      s = fmaf(__uint_as_float(dw[i] << 16), __uint_as_float(ow[i] << 16), s);
+      s = fmaf(__uint_as_float(dw[i] & 0xFFFF0000u), __uint_as_float(ow[i] & 0xFFFF0000u), s);
+    }
+  }
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  if (r < nrows && j == 0) {
+    nd[r] = -s * inv_dscale;
+    nlse2[r] = -lse[r] * 1.4426950408889634f;
+  }
+}
+
+template <int DROP, int HD>
+__global__ __launch_bounds__(512, 2) void attn_bwd_fused_mfma(const bf16_t* __restrict__ qkv, long long ld,
+                                                              const int32_t* __restrict__ seg,
+                                                              const bf16_t* __restrict__ dy, long long lddy,
+                                                              const float* __restrict__ ndrow,
+                                                              const float* __restrict__ nlse2,
+                                                              float* __restrict__ dq_acc, int nq32,
+                                                              bf16_t* __restrict__ dqkv, long long lddq, int T, int H,
+                                                              int KV, int window, float dscale, float scale,
+                                                              const uint32_t* __restrict__ qmask, int wpr,
+                                                              float* __restrict__ bpart, long long ldp,
+                                                              const float* __restrict__ rcos,
+                                                              const float* __restrict__ rsin) {
+  using namespace fa;
+  static_assert(DROP == 0 || DROP == 2, "fused backward: keep bits from the forward's words");
+  constexpr int hd = HD;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BUF = fb_buf(DROP);
+  constexpr int NV = 3 + (DROP == 2 ? 1 : 0);  // DMAs per wave and ring stage
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int bk = blockIdx.x, b = bk / KV, kvh = bk % KV;
+  const int rep = H / KV;
+  const long long rowbase = (long long)b * T;
+  const long long koff = (long long)H * hd + (long long)kvh * hd;
+  const long long voff = (long long)(H + KV) * hd + (long long)kvh * hd;
+  const float c = scale * 1.4426950408889634f;  // K is pre-multiplied by it (exp2 domain)
+  const float kscale = DROP ? scale * dscale : scale;
+  const float qscale = kscale;
+  // MHA without RoPE: the last key block of each tile stores dQ itself, and the q-bias partials are
+  // sum_key (sum_q dS[q][key]) K[key] (no per-query factor to apply); else dq_acc + the finish pass
+  const bool direct = !rcos && rep == 1;
+  const float vsc = DROP ? dscale : 1.0f;
+  constexpr int nks = (hd + 15) >> 4;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)smem;
+  const uint32_t ring_l = lds0, kimg_l = lds0 + 3 * BUF + 2 * FB_DSB;
+  char* const dsb = smem + 3 * BUF;
+  const char* const kimg = dsb + 2 * FB_DSB;
+  const PieceDma qsrc = piece_dma_src(qkv + rowbase * ld, ld, T, hd, wave_u, lane);
+  const PieceDma dsrc = piece_dma_src(dy + rowbase * lddy, lddy, T, hd, wave_u, lane);
+  const uint32_t qstride = (uint32_t)(KT * ld * 2), dstride = (uint32_t)(KT * lddy * 2);
+  const uint32_t kcol = (uint32_t)((H + kvh) * hd * 2);
+  constexpr uint32_t OORD = 0x80000000u;  // past every record: the DMA writes 0
+  const long long bh0 = (long long)b * H * T;  // (b, head 0, query 0) of the per-query rows
+  const float* rowsrc = wave_u == 0 ? nlse2 : ndrow;
+  const __amdgpu_buffer_rsrc_t rrow =
+      wave_u < 2 ? __builtin_amdgcn_make_buffer_rsrc((void*)(rowsrc + bh0), (short)0, H * T * 4, 0x00020000)
+                 : __builtin_amdgcn_make_buffer_rsrc((void*)(seg ? seg + rowbase : nullptr), (short)0,
+                                                     seg ? T * 4 : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rqm = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(DROP == 2 ? qmask + bh0 * wpr : nullptr), (short)0, DROP == 2 ? H * T * wpr * 4 : 0, 0x00020000);
+  // -lse2 | nd | seg rows by waves 0 / 1 / 2; waves 3-7 load the seg row again into a slot nothing reads
+  const uint32_t row_lds = (uint32_t)(2 * IMG + (wave_u < 3 ? wave_u : 3) * 64 * 4);
+  const RowOff ro = row_offsets(lane);
+  const TrOff to = tr_offsets(lane);
+  // this lane's dS^T image row (key 32 wave + (lane & 31) of the block) and its XOR swizzle group;
+  // its 8-byte stores go to columns 8 ch + 4 (lane >> 5) .. + 3
+  const int srow = 32 * (wave & 1) + (lane & 31);
+  const int sg = ((srow >> 1) & 7) ^ (((srow >> 1) & 1) << 2);
+  const uint32_t sbase = (uint32_t)((wave >> 1) * IMG + srow * 128 + 8 * (lane >> 5));
+  const int nkb = (T + FB_KEYS - 1) / FB_KEYS;
+  const int ny = (T + 127) / 128;
+  auto qt_end_of = [&](int kb) {
+    const int qe = window > 0 ? min(T, kb * FB_KEYS + FB_KEYS - 1 + window) : T;
+    return (qe - 1) / KT;
+  };
+  struct Cur {
+    int h2, qt;
+  };
+  // the previous iteration's tile, finished (dQ) by waves 0-3 in the next iteration
+  struct Prev {
+    int h2, qt, first, last;  // first / last key block that visits the tile
+  };
+  for (int kb = 0; kb < nkb; ++kb) {
+    const int kt0 = kb * FB_KEYS, kw0 = kt0 + wave * 32;
+    const int mykey = kw0 + (lane & 31);
+    const bool kok = mykey < T;
+    const bf16_t* krow = qkv + (rowbase + (kok ? mykey : 0)) * ld + koff;
+    const bf16_t* vrow = qkv + (rowbase + (kok ? mykey : 0)) * ld + voff;
+    v8bf kf[4], vf[4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[ks] = scale_frag(frag_global(krow, kok, ks, hd, lane), c);
+      vf[ks] = frag_global(vrow, kok, ks, hd, lane);
+    }
+    // the lane's key bit in a pair-split word: key 2c -> bit c, key 2c+1 -> bit 16 + c
+    const uint32_t kpos = (uint32_t)(((mykey & 31) >> 1) + 16 * (mykey & 1));
+    v16f dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
+    float dscol = 0.f;  // (direct, bias) sum over the block's queries of dS/dscale for the lane's key
+    const int qt_begin = kt0 / KT, qt_end = qt_end_of(kb);
+    const int total = (qt_end - qt_begin + 1) * rep;
+    const int qt_end_prev = kb > 0 ? qt_end_of(kb - 1) : -1;  // tiles <= it were visited by block kb-1
+    const int mw_idx = kt0 / 32 + wave;  // this wave's key word of a query's keep bits
+    auto next_of = [&](Cur cu) { return cu.qt < qt_end ? Cur{cu.h2, cu.qt + 1} : Cur{cu.h2 + 1, qt_begin}; };
+    auto stage_dma = [&](Cur cu, int nb) {
+      const uint32_t buf = ring_l + nb * BUF;
+      piece_dma(buf, qsrc, cu.qt * qstride + (uint32_t)(cu.h2 * hd * 2), wave_u);
+      piece_dma(buf + IMG, dsrc, cu.qt * dstride + (uint32_t)(cu.h2 * hd * 2), wave_u);
+      const int q = cu.qt * KT + lane;
+      dma4(rrow, buf + row_lds, q < T ? (uint32_t)(((wave_u < 2 ? cu.h2 * T : 0) + q) * 4) : OORD);
+      if constexpr (DROP == 2)
+        dma4(rqm, buf + (uint32_t)(2 * IMG + 4 * 64 * 4 + wave_u * 64 * 4),
+             (q < T && mw_idx < wpr)
+                 ? (uint32_t)((((cu.h2 * (wpr >> 1) + (mw_idx >> 1)) * T + q) * 2 + (mw_idx & 1)) * 4)
+                 : OORD);
+    };
+    // the block's K image (rows kt0 .. kt0 + 255, unscaled) for the dQ product: 4 pieces per wave
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      piece_dma(kimg_l + i * IMG, qsrc, (uint32_t)((kt0 + 64 * i) * ld * 2) + kcol, wave_u);
+    Cur cur{kvh * rep, qt_begin};
+    Cur n1 = next_of(cur);
+    Cur n2 = next_of(n1);
+    stage_dma(cur, 0);
+    if (total > 1) {
+      stage_dma(n1, 1);
+      dma_wait<NV>();
+    } else {
+      dma_wait<0>();
+    }
+    __syncthreads();
+    Prev pv{0, 0, 0, 0};
+    bool have_prev = false;
+    // waves 0-3: the dq_acc block of tile (h2, qt) this wave owns -- query half w >> 1, head dims
+    // 32 (w & 1) + acc_row(r): element r at + ((r & 3) + 8 (r >> 2)) * 32
+    auto dq_dst = [&](int h2, int qt) {
+      return dq_acc + dqa_off((long long)b * H + h2, nq32, qt * 2 + (wave_u >> 1), (wave_u & 1) * 32 + 4 * (lane >> 5)) +
+             (lane & 31);
+    };
+    // its old value, loaded at the end of the tile's own iteration (after the tile's phase A): the
+    // load latency runs under the barrier and the other waves' work instead of stalling phase B.
+    // Every wave loads on every iteration (waves 4-7 and first visits a line they ignore), so the
+    // registers are written on every path and no value of them lives through phase A.
+    v16f oldv;
+    // waves 0-3: dQ^T block of tile pv from the dS^T images, accumulated onto oldv.  Straight-line
+    // (inactive key waves wrote zero rows), operand reads one 4-k-step group ahead of the MFMAs
+    auto phase_b = [&](const char* dsimg, const Prev& p) __attribute__((always_inline)) {
+      const int qb = wave_u >> 1, cb = wave_u & 1;
+      const uint32_t ka0 = cb ? to.o[1][0] : to.o[0][0], ka1 = cb ? to.o[1][1] : to.o[0][1];
+      const uint32_t sb0 = qb ? to.o[1][0] : to.o[0][0], sb1 = qb ? to.o[1][1] : to.o[0][1];
+      float* dst = dq_dst(p.h2, p.qt);
+      v16f acc = p.first ? zero16() : oldv;  // the running sum, landed during the barrier
+      v8bf fa[2][4], fb[2][4];
+      auto rd = [&](int g) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kk = 4 * g + i, rb = 32 * ((kk >> 1) & 1), st = kk & 1;
+          fa[g & 1][i] = frag_tr_p(kimg + g * IMG, ka0, ka1, rb, st);
+          fb[g & 1][i] = frag_tr_p(dsimg + g * IMG, sb0, sb1, rb, st);
+        }
+      };
+      rd(0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (g < 3) rd(g + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (FB_DIAG != 1) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[g & 1][i], fb[g & 1][i], acc, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (!p.last || !direct) {  // a later key block adds to it (or the finish pass converts it)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * 32] = acc[r];
+      } else if (cb * 32 < hd) {  // the tile's last key block: dQ = qscale (dS/dscale . K) into dqkv
+        const int q = p.qt * KT + qb * 32 + (lane & 31);
+        const bool qok = q < T;
+        bf16_t* drow = dqkv + (rowbase + (qok ? q : 0)) * lddq + (long long)p.h2 * hd + cb * 32;
+        store_blk16(drow, acc, qscale, qok, hd - cb * 32 < 32 ? hd - cb * 32 : 32, lane);
+      }
+    };
+    // one iteration on ring buffer CUR (compile-time: every image read is lane offset + immediate)
+    auto iter = [&](auto cur_c, int it) __attribute__((always_inline)) {
+      constexpr int CUR = decltype(cur_c)::value;
+      const char* buf = smem + CUR * BUF;
+      const char* Qi = buf;
+      const char* Di = buf + IMG;
+      const float* lse2s = (const float*)(buf + 2 * IMG);
+      const float* nds = lse2s + 64;
+      const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
+      const uint32_t* mws = (const uint32_t*)(buf + 2 * IMG + 4 * 64 * 4) + wave * 64;
+      // the dS^T store offsets are rebuilt each iteration from (sbase, sg), which the empty asm makes
+      // opaque: hoisted out of the loop, the eight per-lane offsets would stay live through phase A
+      uint32_t sb_i = sbase;
+      int sg_i = sg;
+      asm volatile("" : "+v"(sb_i), "+v"(sg_i));
+      char* dsw = dsb + (it & 1) * FB_DSB + sb_i;
+      const bool more1 = it + 1 < total, more2 = it + 2 < total;
+      // the previous tile's dQ first: its dq_acc loads and stores precede this iteration's DMAs in
+      // vmcnt order, so the counted waits below leave exactly the newest stage in flight
+      if (FB_DIAG != 2 && wave_u < 4 && have_prev) phase_b(dsb + ((it - 1) & 1) * FB_DSB, pv);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more2) stage_dma(n2, (CUR + 2) % 3);  // that buffer was last read before the previous barrier
+      const int q0 = cur.qt * KT;
+      const int qlast = min(T - 1, q0 + KT - 1);
+      auto lo_at = [&](int i) { return window > 0 ? max(los[i], q0 + i - window + 1) : los[i]; };
+      const int lo0 = lo_at(0);
+      // wave activity: some query of the tile sees some key of the wave (lo is monotone in q)
+      const bool active = (qlast >= kt0 + 32 * wave_u) && (lo0 <= kt0 + 32 * wave_u + 31);
+      auto phase_sdp = [&](int qb, v16f& s, v16f& dp, v16f& nd) __attribute__((always_inline)) {
+#pragma unroll
+        for (int rg = 0; rg < 16; rg += 4) {
+          const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
+          nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
+          const float4 l4 = *(const float4*)(lse2s + qb * 32 + acc_row(rg, lane));
+          s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
+        }
+        dp = nd;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          if (ks < nks) {
+            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Qi, ro, qb * 32, ks), kf[ks], s, 0, 0, 0);
+            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
+          }
+        }
+      };
+      auto phase_ds = [&](int qb, auto full_c, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1,
+                          v8bf& sb0, v8bf& sb1) __attribute__((always_inline)) {
+        bool full;
+        if constexpr (std::is_same_v<decltype(full_c), bool>) full = full_c;
+        else full = decltype(full_c)::value;
+        if (!full) {
+#pragma unroll
+          for (int rg = 0; rg < 16; rg += 4) {
+            const int qi = qb * 32 + acc_row(rg, lane);
+            const int4 lo4 = *(const int4*)(los + qi);
+            const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int q = q0 + qi + u;
+              const int lq = window > 0 ? max(lov[u], q - window + 1) : lov[u];
+              s[rg + u] = ((mykey > q) | (mykey < lq) | (q >= T)) ? -INFINITY : s[rg + u];
+            }
+          }
+        }
+        v16f pd;
+#pragma unroll
+        for (int rg = 0; rg < 16; rg += 4) {
+          const int qi = qb * 32 + acc_row(rg, lane);
+          uint4 mw4 = make_uint4(0, 0, 0, 0);
+          if constexpr (DROP == 2) mw4 = *(const uint4*)(mws + qi);
+          const uint32_t mwv[4] = {mw4.x, mw4.y, mw4.z, mw4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int r = rg + u;
+            const float p = __builtin_amdgcn_exp2f(s[r]);
+            float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
+            if constexpr (DROP == 2) {
+              const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
+              pdr = __uint_as_float(__float_as_uint(p) & m);
+              s[r] = p * bsel(m, dp[r], nd[r]);
+            } else {
+              s[r] = p * dp[r];
+            }
+            pd[r] = pdr;
+          }
+        }
+        pb0 = pack_b(pd, 0); pb1 = pack_b(pd, 1);
+        sb0 = pack_b(s, 0); sb1 = pack_b(s, 1);
+      };
+      struct TrFr { v8bf d[4], q[4]; };
+      auto tr_frags = [&](int qb, TrFr& f) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < (hd > 32 ? 4 : 2); ++i) {
+          f.d[i] = frag_tr_o(Di, to, qb * 32, i & 1, i >> 1);
+          f.q[i] = frag_tr_o(Qi, to, qb * 32, i & 1, i >> 1);
+        }
+      };
+      auto phase_dkdv = [&](const TrFr& f, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
+                            __attribute__((always_inline)) {
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[0], pb0, dv0, 0, 0, 0);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[1], pb1, dv0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[0], sb0, dk0, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[1], sb1, dk0, 0, 0, 0);
+        if constexpr (hd > 32) {
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[2], pb0, dv1, 0, 0, 0);
+          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[3], pb1, dv1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[2], sb0, dk1, 0, 0, 0);
+          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[3], sb1, dk1, 0, 0, 0);
+        }
+      };
+      auto body = [&](auto full) __attribute__((always_inline)) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+          v16f s, dp, nd;
+          v8bf x0, x1, x2, x3;
+          TrFr f;
+          phase_sdp(qb, s, dp, nd);
+          tr_frags(qb, f);
+          __builtin_amdgcn_sched_barrier(0);
+          phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
+          if (direct && bpart) {
+            float t = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t += s[r];
+            dscol += t;
+          }
+          // dS^T rows of this wave's keys: x2 = queries 4h + {0..3, 8..11}, x3 = 4h + {16..19, 24..27}
+          // of the half, i.e. chunks 4 qb + 0..3 of the image row, 8 bytes at 8 (lane >> 5) in each
+          const v4u_a w0 = __builtin_bit_cast(v4u_a, x2), w1 = __builtin_bit_cast(v4u_a, x3);
+          *(uint2*)(dsw + 16 * ((4 * qb + 0) ^ sg_i)) = make_uint2(w0[0], w0[1]);
+          *(uint2*)(dsw + 16 * ((4 * qb + 1) ^ sg_i)) = make_uint2(w0[2], w0[3]);
+          *(uint2*)(dsw + 16 * ((4 * qb + 2) ^ sg_i)) = make_uint2(w1[0], w1[1]);
+          *(uint2*)(dsw + 16 * ((4 * qb + 3) ^ sg_i)) = make_uint2(w1[2], w1[3]);
+          phase_dkdv(f, x0, x1, x2, x3);
+        }
+      };
+      if (active) {
+        const bool full = (q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0);
+        body(full);
+      } else {  // no visible pair: zero dS^T rows, so the dQ product runs straight through
+#pragma unroll
+        for (int c8 = 0; c8 < 8; ++c8) *(uint2*)(dsw + 16 * (c8 ^ sg_i)) = make_uint2(0u, 0u);
+      }
+      pv = Prev{cur.h2, cur.qt, cur.qt > qt_end_prev ? 1 : 0, (cur.qt >> 2) == kb ? 1 : 0};
+      have_prev = true;
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads (and their 16 registers) out of phase A
+      {
+        const float* src = wave_u < 4 ? dq_dst(cur.h2, cur.qt) : dq_acc + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) oldv[r] = src[((r & 3) + 8 * (r >> 2)) * 32];
+      }
+      // n1's data (issued an iteration ago) landed; n2's DMAs -- and the 16 oldv loads issued after
+      // them -- may still be in flight
+      if (more1) {
+        if (more2) dma_wait<NV + 16>();
+        else dma_wait<16>();
+      }
+      cur = n1;
+      n1 = n2;
+      n2 = next_of(n2);
+      // raw barrier: no vmcnt(0) (n2's DMAs stay in flight); the dS^T stores and this wave's image
+      // reads retired first
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    for (int it = 0; it < total; it += 3) {
+      iter(std::integral_constant<int, 0>{}, it);
+      if (it + 1 < total) iter(std::integral_constant<int, 1>{}, it + 1);
+      if (it + 2 < total) iter(std::integral_constant<int, 2>{}, it + 2);
+    }
+    if (wave_u < 4) phase_b(dsb + ((total - 1) & 1) * FB_DSB, pv);  // the last tile's dQ
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the block
+    __syncthreads();  // the K / dS^T images are free (bias scratch, the next block's K image)
+    if (rcos) {  // RoPE: dK w.r.t. the rotated k, rotated back at the key's position
+      const size_t ro2 = (size_t)(kok ? mykey : 0) * (hd / 2);
+      rope_inv_blocks<hd>(dk0, dk1, rcos + ro2, rsin + ro2, lane >> 5);
+    }
+    {
+      bf16_t* kr = dqkv + (rowbase + (kok ? mykey : 0)) * lddq + koff;
+      bf16_t* vr = dqkv + (rowbase + (kok ? mykey : 0)) * lddq + voff;
+      store_blk16(kr, dk0, kscale, kok, hd < 32 ? hd : 32, lane);
+      store_blk16(vr, dv0, vsc, kok, hd < 32 ? hd : 32, lane);
+      if (hd > 32) {
+        store_blk16(kr + 32, dk1, kscale, kok, hd - 32, lane);
+        store_blk16(vr + 32, dv1, vsc, kok, hd - 32, lane);
+      }
+    }
+    if (bpart) {  // k / v (and q) bias partials of the block into row 2 kb of the batch's 128-row tiles
+      float* red = (float*)smem;
+      const float vk = colsum_wg8(dk0, dk1, kscale, kok, red, wave, lane, tid);
+      const float vv = colsum_wg8(dv0, dv1, vsc, kok, red, wave, lane, tid);
+      float vq = 0.f;
+      if (direct) {  // sum_key dscol[key] K[key][d], K from the block's image (raw bf16)
+        uint32_t kr_o = (uint32_t)((wave >> 1) * IMG + srow * 128 + 8 * (lane >> 5));
+        int sg_k = sg;
+        asm volatile("" : "+v"(kr_o), "+v"(sg_k));  // (not hoisted out of the key-block loop)
+        const char* krow_l = kimg + kr_o;
+        v16f x0, x1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int cbk = 0; cbk < 2; ++cbk) {  // head dims 32 cbk + 8 j + 4 (lane >> 5) .. + 3
+            const int ch = 4 * cbk + j;
+            const uint2 kv = *(const uint2*)(krow_l + 16 * (ch ^ sg_k));
+            const float k4[4] = {__uint_as_float(kv.x << 16), __uint_as_float(kv.x & 0xFFFF0000u),
+                                 __uint_as_float(kv.y << 16), __uint_as_float(kv.y & 0xFFFF0000u)};
+#pragma unroll
+            for (int t = 0; t < 4; ++t) (cbk ? x1 : x0)[4 * j + t] = dscol * k4[t];
+          }
+        vq = colsum_wg8(x0, x1, qscale, kok, red, wave, lane, tid);
+      }
+      float* dst = bpart + ((long long)b * ny + 2 * kb) * ldp;
+      const long long qoff = (long long)kvh * hd;  // (direct: rep == 1, the query head is kvh)
+      if (tid < hd) {
+        dst[koff + tid] = vk;
+        dst[voff + tid] = vv;
+        if (direct) dst[qoff + tid] = vq;
+        if (2 * kb + 1 < ny) {  // the block's second 128-row tile: its sums are in row 2 kb
+          dst[ldp + koff + tid] = 0.f;
+          dst[ldp + voff + tid] = 0.f;
+          if (direct) dst[ldp + qoff + tid] = 0.f;
+        }
+      }
+    }
+  }
+}
+
+// dq_acc (fp32 sums of dS/dscale . K over all keys, fa::dqa_off layout) -> the bf16 dqkv q columns:
+// x qscale, RoPE inverse at the query's position (rcos != NULL), and the q-bias partial row of the
+// 128-query tile (column sums of the unrounded values).  WG: one (b, h) x 128 queries.
+template <int HD>
+__global__ __launch_bounds__(256) void attn_dq_finish_kernel(const float* __restrict__ dq_acc, int nq32,
+                                                             bf16_t* __restrict__ dqkv, long long lddq, int T, int H,
+                                                             float qscale, float* __restrict__ bpart, long long ldp,
+                                                             const float* __restrict__ rcos,
+                                                             const float* __restrict__ rsin) {
+  constexpr int hd = HD, PITCH = 65;
+  __shared__ float t[128 * PITCH];
+  const int tid = threadIdx.x;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int q0 = blockIdx.y * 128;
+  // 4 query blocks of 32 x 64 head dims x 32 queries: 8 float4 per thread, coalesced
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = i * 256 + tid;             // float4 index in the 128-query slab
+    const int blk = e >> 9, d = (e >> 3) & 63, q4 = (e & 7) * 4;
+    const int q32 = (q0 >> 5) + blk;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (q32 < nq32) v = *(const float4*)(dq_acc + fa::dqa_off(bh, nq32, q32, d) + q4);
+    float* row = t + (blk * 32 + q4) * PITCH + d;
+    row[0] = v.x; row[PITCH] = v.y; row[2 * PITCH] = v.z; row[3 * PITCH] = v.w;
+  }
+  __syncthreads();
+  {
+    // thread (query tid >> 1, half tid & 1): pairs i of [half hd/4, (half + 1) hd/4), dims i, i + hd/2
+    const int ql = tid >> 1, half = tid & 1, q = q0 + ql;
+    float* row = t + ql * PITCH;
+    constexpr int hh = hd / 2, np = hd / 4;
+    const float* cs = rcos ? rcos + (size_t)(q < T ? q : 0) * hh : nullptr;
+    const float* sn = rcos ? rsin + (size_t)(q < T ? q : 0) * hh : nullptr;
+#pragma unroll
+    for (int k = 0; k < np; ++k) {
+      const int i = half * np + k;
+      const float g = row[i], gp = row[i + hh];
+      if (cs) {
+        row[i] = qscale * fmaf(cs[i], g, sn[i] * gp);
+        row[i + hh] = qscale * fmaf(cs[i], gp, -sn[i] * g);
+      } else {
+        row[i] = qscale * g;
+        row[i + hh] = qscale * gp;
+      }
+    }
+  }
+  __syncthreads();
+  const int nq = min(128, T - q0);
+  if (bpart && tid < hd) {  // the q-bias partial of this 128-query tile (fixed order)
+    float a = 0.f, c2 = 0.f;
+    int k = 0;
+    for (; k + 1 < nq; k += 2) {
+      a += t[k * PITCH + tid];
+      c2 += t[(k + 1) * PITCH + tid];
+    }
+    if (k < nq) a += t[k * PITCH + tid];
+    bpart[((long long)b * gridDim.y + blockIdx.y) * ldp + (long long)h * hd + tid] = a + c2;
+  }
+  // bf16 rows, 16 B per thread-chunk
+  constexpr int CH = hd / 8;
+  for (int e = tid; e < 128 * CH; e += 256) {
+    const int ql = e / CH, ch = e - ql * CH;
+    if (ql >= nq) continue;
+    const float* src = t + ql * PITCH + ch * 8;
+    uint4 o;
+    o.x = fa::pk2bf(src[0], src[1]);
+    o.y = fa::pk2bf(src[2], src[3]);
+    o.z = fa::pk2bf(src[4], src[5]);
+    o.w = fa::pk2bf(src[6], src[7]);
+    *(uint4*)(dqkv + ((long long)b * T + q0 + ql) * lddq + (long long)h * hd + ch * 8) = o;
+  }
+}
+
 // ----------------------------------------------------------------------------
 static inline bool attn_mfma_supported(int hd, long long ld_in, long long ld_out) {
   return (hd == 32 || hd == 48 || hd == 64) && (ld_in % 8 == 0) && (ld_out % 8 == 0);
@@ -1217,12 +1826,77 @@ static inline int attn_fwd_mfma_launch(const bf16_t* qkv, long long ld, const in
   return CG_OK;
 }
 
+// fused backward workspace after the two per-query rows: dq_acc, [B H][Tp / 32][64][32] fp32
+static inline int attn_dq_nq32(int T) { return cg_cdiv(T, 64) * 2; }
+static inline size_t attn_dq_acc_floats(int B, int T, int H) {
+  return (size_t)B * H * attn_dq_nq32(T) * 64 * 32;
+}
+// the fused pass when every CU gets a (batch, kv head) workgroup (it runs one per CU); the
+// two-kernel pass spreads small batches over more workgroups.  Hash-in-kernel dropout (no keep
+// words) stays on the two-kernel pass.
+static inline bool attn_bwd_fused_ok(int algo, int B, int KV, int mode) {
+  if (mode == 1 || algo == CG_ATTN_BWD_SPLIT) return false;
+  if (algo == CG_ATTN_BWD_FUSED) return true;
+  (void)B; (void)KV;
+  return false;  // AUTO: the split pass until the fused one measures faster
+}
+
+static inline int attn_bwd_fused_launch(const bf16_t* qkv, long long ld, const int32_t* seg, const bf16_t* y,
+                                        long long ldy, const bf16_t* dy, long long lddy, const float* lse,
+                                        float* ws, bf16_t* dqkv, long long lddq, int B, int T, int H, int KV, int hd,
+                                        int window, float dscale, float scale, const uint32_t* dmask, float* bpart,
+                                        long long ldp, hipStream_t s, const float* rcos, const float* rsin) {
+  const long long nbt = (long long)B * H * T;
+  float* nd = ws;
+  float* nlse2 = ws + nbt;
+  float* dq_acc = ws + 2 * nbt;
+  const int nq32 = attn_dq_nq32(T);
+  const int wpr = attn_drop_wpr(T);
+  const int mode = dmask ? 2 : 0;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3(cg_cdiv(nbt, 32)), dim3(256), 0, s, dy, lddy, y, ldy, lse, nd, nlse2,
+                     T, H, hd, mode ? 1.0f / dscale : 1.0f, nbt);
+  CG_LAUNCH_CHECK();
+  const double tri = 2.0 * (double)B * H * hd * ((double)T * (T + 1) / 2.0);
+  const int sh = fa::fb_lds(mode);
+  cg_probe_begin(CG_PROBE_ATTN_BWD, s);
+#define FB(D, HDv)                                                                                              \
+  do {                                                                                                          \
+    cg_func_lds((const void*)attn_bwd_fused_mfma<D, HDv>, sh);                                                  \
+    hipLaunchKernelGGL((attn_bwd_fused_mfma<D, HDv>), dim3(B * KV), dim3(512), sh, s, qkv, ld, seg, dy, lddy, nd, \
+                       nlse2, dq_acc, nq32, dqkv, lddq, T, H, KV, window, dscale, scale, dmask, wpr, bpart, ldp,  \
+                       rcos, rsin);                                                                             \
+  } while (0)
+#define FBH(D) if (hd == 64) FB(D, 64); else if (hd == 48) FB(D, 48); else FB(D, 32)
+  if (mode == 2) { FBH(2); } else { FBH(0); }
+#undef FBH
+#undef FB
+  cg_probe_end(CG_PROBE_ATTN_BWD, s, 5.0 * tri);  // S, dP recomputed + dV, dK, dQ
+  CG_LAUNCH_CHECK();
+  if (!rcos && H == KV) return CG_OK;  // MHA without RoPE: the last key block of each tile stored dQ
+  const float qscale = mode ? scale * dscale : scale;
+  const dim3 gf(B * H, cg_cdiv(T, 128));
+  if (hd == 64)
+    hipLaunchKernelGGL(attn_dq_finish_kernel<64>, gf, dim3(256), 0, s, dq_acc, nq32, dqkv, lddq, T, H, qscale, bpart,
+                       ldp, rcos, rsin);
+  else if (hd == 48)
+    hipLaunchKernelGGL(attn_dq_finish_kernel<48>, gf, dim3(256), 0, s, dq_acc, nq32, dqkv, lddq, T, H, qscale, bpart,
+                       ldp, rcos, rsin);
+  else
+    hipLaunchKernelGGL(attn_dq_finish_kernel<32>, gf, dim3(256), 0, s, dq_acc, nq32, dqkv, lddq, T, H, qscale, bpart,
+                       ldp, rcos, rsin);
+  CG_LAUNCH_CHECK();
+  return CG_OK;
+}
+
 static inline int attn_bwd_mfma_launch(const bf16_t* qkv, long long ld, const int32_t* seg, const bf16_t* y,
                                        long long ldy, const bf16_t* dy, long long lddy, const float* lse,
                                        float* delta, bf16_t* dqkv, long long lddq, int B, int T, int H, int KV,
                                        int hd, int window, uint32_t seed, uint32_t thr, float dscale, float scale,
                                        const uint32_t* dmask, float* bpart, long long ldp, hipStream_t s,
-                                       const float* rcos = nullptr, const float* rsin = nullptr) {
+                                       const float* rcos = nullptr, const float* rsin = nullptr, int algo = 0) {
+  if (attn_bwd_fused_ok(algo, B, KV, thr ? (dmask ? 2 : 1) : 0))
+    return attn_bwd_fused_launch(qkv, ld, seg, y, ldy, dy, lddy, lse, delta, dqkv, lddq, B, T, H, KV, hd, window,
+                                 dscale, scale, thr ? dmask : nullptr, bpart, ldp, s, rcos, rsin);
   dim3 gq(B * H, cg_cdiv(T, 128));
   const int wpr = attn_drop_wpr(T);
   float* nlse2 = delta + (long long)B * H * T;  // second half of the workspace

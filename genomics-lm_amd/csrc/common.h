@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <mutex>
 #include "../../include/codonlm_hip.h"
 #include "probe.h"
 
@@ -150,6 +151,26 @@ __device__ __forceinline__ float dgelu_fast(float x) {
 __device__ __forceinline__ int cg_xcd_remap(int orig, int nwg) {
   const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute belongs to
+// the kernel on the CURRENT device, so a process that drives several GPUs sets it on each of them
+static inline void cg_func_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static const void* fns[512];
+  static int devs[512], lds[512], n = 0;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  for (int i = 0; i < n; ++i)
+    if (fns[i] == fn && devs[i] == dev && lds[i] >= bytes) return;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (n < 512) {
+    fns[n] = fn;
+    devs[n] = dev;
+    lds[n] = bytes;
+    ++n;
+  }
 }
 
 #define CG_LAUNCH_CHECK()                                   \

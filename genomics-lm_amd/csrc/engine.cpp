@@ -35,7 +35,8 @@ struct Dims {
 bool dims_of(const cg_model_cfg* c, Dims& D) {
   if (!c || c->n_embd <= 0 || c->n_head <= 0 || c->n_embd % c->n_head) return false;
   // engine options (zero = defaults): out-of-range values are an error, not a silent default
-  if (c->opts.dw_group < 0 || c->opts.dw_ksplit < 0 || c->opts.dw_ksplit > 3 || c->opts.dw_plan_tokens < 0)
+  if (c->opts.dw_group < 0 || c->opts.dw_ksplit < 0 || c->opts.dw_ksplit > 3 || c->opts.dw_plan_tokens < 0 ||
+      c->opts.attn_bwd_algo < CG_ATTN_BWD_AUTO || c->opts.attn_bwd_algo > CG_ATTN_BWD_FUSED)
     return false;
   D.V = c->vocab_size;
   D.Vp = (int)rup(c->vocab_size, 16);
@@ -1171,9 +1172,10 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     const float* rc_sin = rope_in ? m->rope_sin : nullptr;
     int rc = CG_EUNSUPPORTED;
     if (!D.rope || rope_in)
-      rc = cg_attn_bwd_rope(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv,
-                            C.B, C.T, D.H, D.KV, D.hd, m->window, site_seed(seed, l, SITE_ATTN), p, dmask_b, sl.bpart,
-                            D.Nqkv, rc_cos, rc_sin, A.delta, A.nb.delta, C.s);
+      rc = cg_attn_bwd_algo(m->cfg.opts.attn_bwd_algo, C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall,
+                            d, a.lse, sl.dqkv, D.Nqkv, C.B, C.T, D.H, D.KV, D.hd, m->window,
+                            site_seed(seed, l, SITE_ATTN), p, dmask_b, sl.bpart, D.Nqkv, rc_cos, rc_sin, A.delta,
+                            A.nb.delta, C.s);
     const bool fused_bias = rc == CG_OK;
     if (rc == CG_EUNSUPPORTED) {
       rc = cg_attn_bwd(C.dt, a.qkv, D.Nqkv, (const int32_t*)segp, a.y, d, A.dsmall, d, a.lse, sl.dqkv, D.Nqkv, C.B,
@@ -1413,4 +1415,4 @@ extern "C" size_t cg_struct_bytes(const char* name) {
   return 0;
 }
 
-extern "C" const char* cg_version(void) { return "codonlm_hip 0.4 gfx950"; }
+extern "C" const char* cg_version(void) { return "codonlm_hip 0.5 gfx950"; }

@@ -228,7 +228,8 @@ int cg_attn_fwd_keep(int dtype, const void* qkv, long long ldqkv, const int32_t*
 int cg_attn_probs(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart, const float* lse,
                   float* out, int B, int T, int H, int KV, int hd, int window, void* stream);
 /* backward: writes dqkv (dtype) for q,k,v column blocks.  ws: ws_bytes >= cg_attn_bwd_workspace()
- * bytes (else CG_EINVAL).
+ * bytes (else CG_EINVAL; 2 B H T + 4096 B H ceil(T/64) floats: the per-query rows and the fused pass's
+ * dQ accumulator).
  * bias_part (optional, bf16 MFMA path only -- CG_EUNSUPPORTED otherwise): fp32 column sums of
  * dqkv (before bf16 rounding) per (batch, 128-row tile), rows b*ceil(T/128) + tile, leading dim
  * ld_part >= (H + 2 KV) hd; reduced by cg_colsum_reduce into the q/k/v bias gradients. */
@@ -245,6 +246,24 @@ int cg_attn_bwd(int dtype, const void* qkv, long long ldqkv, const int32_t* segs
  * rope_cos / rope_sin: 16-B aligned fp32 [>= T][hd/2] tables as cg_rope_tab takes; both NULL =
  * cg_attn_bwd.  Tables with a non-MFMA configuration (fp32, hd not 32/48/64): CG_EUNSUPPORTED. */
 int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
+                     const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
+                     void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
+                     uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
+                     long long ld_part, const float* rope_cos, const float* rope_sin, void* ws,
+                     size_t ws_bytes, void* stream);
+/* ABI 0.5: cg_attn_bwd_rope with the bf16 MFMA backward's algorithm chosen per call.
+ *   CG_ATTN_BWD_AUTO  (0): the fused pass when B * KV >= the device's CU count, else the split pass
+ *   CG_ATTN_BWD_SPLIT (1): two kernels -- dQ (S, dP, dQ per query tile), then dK / dV (S, dP, dV,
+ *                          dK per key tile): seven MFMA products per tile
+ *   CG_ATTN_BWD_FUSED (2): one pass per (batch, kv head) -- S, dP, dV, dK and dQ, five products per
+ *                          tile, dQ summed over the key blocks in an fp32 part of ws that only that
+ *                          workgroup writes (no atomics: bitwise reproducible) -- between a row-
+ *                          statistics pre-pass and a pass that writes the bf16 dQ columns
+ * Both replace the autograd of model_tiny_gpt.py:102-131 with the same results up to fp32
+ * summation order.  FUSED needs the bf16 MFMA configuration and, with dropout, drop_mask
+ * (CG_EUNSUPPORTED otherwise); AUTO and SPLIT run every configuration. */
+enum { CG_ATTN_BWD_AUTO = 0, CG_ATTN_BWD_SPLIT = 1, CG_ATTN_BWD_FUSED = 2 };
+int cg_attn_bwd_algo(int algo, int dtype, const void* qkv, long long ldqkv, const int32_t* segstart,
                      const void* y, long long ldy, const void* dy, long long lddy, const float* lse,
                      void* dqkv, long long lddqkv, int B, int T, int H, int KV, int hd, int window,
                      uint32_t drop_seed, float drop_p, const void* drop_mask, float* bias_part,
@@ -375,6 +394,7 @@ typedef struct {
                           /* each block's forward (0: written by the attention forward itself)  */
   int dw_plan_tokens;     /* > 0: plan the grouped dW as for steps of this many tokens (a small  */
                           /* parity step then runs a large step's plan); 0: the step's own B*T  */
+  int attn_bwd_algo;      /* ABI 0.5: CG_ATTN_BWD_* for every block's attention backward (0 auto) */
 } cg_model_opts;
 typedef struct {
   int vocab_size, block_size, n_layer, n_head, n_kv_head, n_embd;
@@ -514,8 +534,9 @@ enum {
   CG_PROBE_ATTN_DQ = 5,      /* attn_bwd_dq_mfma                                   */
   CG_PROBE_ATTN_DKDV = 6,    /* attn_bwd_dkdv_mfma                                 */
   CG_PROBE_GEMM_DW_GROUPED = 7, /* grouped weight-gradient GEMM (gemm_dw_kernel)     */
-  CG_PROBE_GEMM_PERS = 8       /* persistent fwd / dX GEMM (gemm_bf16_pers_kernel, all */
+  CG_PROBE_GEMM_PERS = 8,      /* persistent fwd / dX GEMM (gemm_bf16_pers_kernel, all */
                                /* epilogue specialisations: one kernel class)           */
+  CG_PROBE_ATTN_BWD = 9        /* attn_bwd_fused_mfma (the fused dQ / dK / dV pass)     */
 };
 int cg_probe_enable(int kind);
 /* record 1 of every `every` launches of the probed kernel (default 1 = all); the launch
@@ -541,7 +562,9 @@ size_t cg_struct_bytes(const char* name);
  * the engine-private head_dw_* fields at its end.  ABI 0.4 (round 5): no process-wide setters --
  * cg_gemm_desc.tile / max_wg, cg_dw_group.max_wg and cg_model_cfg.opts replace the cg_set_* /
  * cg_gemm_set_* calls and the environment switches; cg_model_dw_plan takes (B, T) and reports the
- * token split; cg_model.embed_done is gone. */
+ * token split; cg_model.embed_done is gone.  ABI 0.5 (round 6): the fused attention backward --
+ * cg_attn_bwd_algo, cg_model_opts.attn_bwd_algo, CG_PROBE_ATTN_BWD; cg_attn_bwd_workspace also
+ * covers the fused pass's dQ accumulator. */
 const char* cg_version(void);
 
 #ifdef __cplusplus

@@ -18,8 +18,9 @@ reductions.  The oracle's fp32 autograd of a 12-layer T1024 B=2 step takes a few
     sequence (data_loading.py:380-393), so B*T is arbitrary -- B=3, T=T_cfg/3 - 1 gives
     B*T % 64 != 0 through every kernel, the grouped dW's zero-filled last k-step included.
 
-Bounds.  fp32 engine: the north-star 1e-4 (logits relative to the logit scale, loss, and
-every parameter gradient relative to its largest entry).  bf16 engine: bf16 storage of
+Bounds.  fp32 engine: logits within an absolute bound ~5x the error measured at each geometry
+(FP32_LOGIT_ABS, 3e-4 .. 2.5e-3 against logit scales of 116-391), the loss within the north-star
+1e-4, every parameter gradient within 2e-4 of its largest entry.  bf16 engine: bf16 storage of
 weights and activations (8 significant bits, rounding 2^-9 relative per value) with fp32
 accumulation everywhere; through 4-12 residual blocks, the head and the loss that gives
 relative L2 errors of a few 1e-3 (measured at full depth on the MI355X: 1.2-1.9e-3 logits,
@@ -44,6 +45,12 @@ DEV = "cuda"
 LOGIT_REL_L2_BF16 = 5e-3
 GRAD_REL_L2_BF16 = 1.5e-2
 TOL_FP32 = 1e-4
+# fp32 logits, absolute: ~5x the max |dlogit| measured on the MI355X at these full-depth geometries
+# (round 5: C1 5.3e-5, C2 1.7e-4, C3 4.6e-4, C4 4.0e-4, C5 2.4e-4 over plain + ragged), against
+# logit scales of 116-391 (the N(0,1) embeddings) -- i.e. 1.3e-6 relative at worst, where the
+# north star's "1e-4" relative reading would allow 3.9e-2.  The trained-scale (std 0.02) leg with
+# the literal absolute 1e-4 is tests/test_gpu_greedy_neartie.py, at these same depths.
+FP32_LOGIT_ABS = {"C1": 3e-4, "C2": 8e-4, "C3": 2.5e-3, "C4": 2e-3, "C5": 1.2e-3}
 
 # per-GPU microbatch of each config's bench line (bench.py CONFIGS): the dW plan the parity runs take
 BENCH_B = {"C2": 256, "C3": 256, "C4": 32, "C5": 128}
@@ -230,9 +237,9 @@ def test_fp32_engine_matches_oracle(name, variant):
     lg = logits.detach().cpu()
     scale = max(1.0, float(rlogits.abs().max()))
     abs_err = float((lg - rlogits).abs().max())
-    print(f"[{name}-{variant} fp32] max |dlogit| {abs_err:.2e} (bound {TOL_FP32 * scale:.2e} = 1e-4 x max|logit| "
-          f"{scale:.2f}); loss {loss.item():.6f} vs {rloss:.6f}")
-    assert abs_err <= TOL_FP32 * scale, (name, abs_err)
+    print(f"[{name}-{variant} fp32] max |dlogit| {abs_err:.2e} (bound {FP32_LOGIT_ABS[name]:.1e} absolute; "
+          f"max|logit| {scale:.2f}); loss {loss.item():.6f} vs {rloss:.6f}")
+    assert abs_err <= FP32_LOGIT_ABS[name], (name, abs_err)
     assert abs(loss.item() - rloss) <= TOL_FP32 * max(1.0, abs(rloss)), name
     assert abs(total.item() - rtotal) <= TOL_FP32 * max(1.0, abs(rtotal)), name
     # bit-exact greedy ids wherever the oracle's top-2 margin is resolvable at fp32

@@ -23,11 +23,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 GEOM = {
-    # SURVEY §8 C2 - C5 shapes (fewer layers at C3 / C4 / C5 keep the CPU oracle to seconds)
+    # SURVEY §8 C2 - C5 shapes at their full depths (the oracle's fp32 forward takes seconds)
     "c2": dict(n_layer=6, n_head=4, n_embd=256, block_size=512, B=2),
-    "c3": dict(n_layer=4, n_head=8, n_kv_head=4, n_embd=384, block_size=512, use_swiglu=True, use_rope=True, B=2),
-    "c4": dict(n_layer=4, n_head=8, n_embd=512, block_size=1024, B=1),
-    "c5": dict(n_layer=4, n_head=8, n_embd=384, block_size=512, termination_aux=True,
+    "c3": dict(n_layer=10, n_head=8, n_kv_head=4, n_embd=384, block_size=512, use_swiglu=True, use_rope=True, B=2),
+    "c4": dict(n_layer=12, n_head=8, n_embd=512, block_size=1024, B=1),
+    "c5": dict(n_layer=10, n_head=8, n_embd=384, block_size=512, termination_aux=True,
                multi_offset_targets=[2, 4, 8, 16, 32], B=2),
 }
 
@@ -47,7 +47,7 @@ def _check(tag, got, ref, need_ties=True):
           f"argmax differences: {int(diff.sum())}")
     if need_ties:  # the test is only meaningful if near-ties occur at all
         assert margin.min() < 1e-3, tag
-    assert maxd <= 1e-4 * max(1.0, scale), tag
+    assert maxd <= 1e-4, tag  # the north star's 1e-4, absolute (the logits here are O(0.5))
     assert not np.any(diff & ~exempt), (tag, np.argwhere(diff & ~exempt)[:8])
 
 

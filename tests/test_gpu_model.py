@@ -2,8 +2,8 @@
 
 The golden fixtures (tests/golden/*.npz) hold outputs of the real reference TinyGPT
 (src/codonlm/model_tiny_gpt.py) run in the build container.  fp32 mode must match them
-to the north-star tolerance (logits/loss within 1e-4, relative to the logit scale, and
-bit-exact greedy ids); bf16 mode is checked against the same vectors with a bf16 bound.
+to the north-star tolerance (logits within 1e-4 absolute or 5e-6 of the logit scale when that
+is larger, loss within 1e-4, bit-exact greedy ids); bf16 mode is checked against the same vectors with a bf16 bound.
 """
 import math
 
@@ -54,7 +54,10 @@ def test_fp32_forward_matches_reference(case):
     got = logits.cpu().numpy()
     scale = max(1.0, float(np.abs(ref).max()))
     err = float(np.abs(got - ref).max())
-    assert err <= 1e-4 * scale, (err, scale)
+    print(f"[{case} fp32] max |dlogit| {err:.2e}, max |logit| {scale:.2f}")
+    # fp32 against the reference's own fp32 logits: the kernels' summation order only (measured at the
+    # full-depth configs: <= 1.3e-6 of the logit scale); 5e-6 of the scale, absolute floor 1e-4
+    assert err <= max(1e-4, 5e-6 * scale), (err, scale)
     assert abs(loss.item() - float(g["loss"])) <= 1e-4 * max(1.0, abs(float(g["loss"])))
     # greedy next-codon ids bit-exact wherever the reference's top-2 margin is resolvable
     greedy = got.argmax(-1)

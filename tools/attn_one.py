@@ -1,6 +1,7 @@
 """One forward + backward of the C4 attention (dropout 0.1, SEP segments), for PMC passes.
 Uses the engine's path: keep bits written by the forward (cg_attn_fwd_keep); ATTN_MASK=1: made by
-cg_attn_drop_mask first (the round-2 path), ATTN_HASH=1: hashed in every kernel."""
+cg_attn_drop_mask first (the round-2 path), ATTN_HASH=1: hashed in every kernel.  The backward runs
+once per algorithm (split: dQ + dK/dV kernels; fused: attn_bwd_fused_mfma), so one PMC pass counts both."""
 import os
 import sys
 from pathlib import Path
@@ -22,6 +23,9 @@ for _ in range(2):
     else:
         y, lse, mask = ops.attn_fwd_keep(qkv, seg, B, T, H, H, hd, 5, 0.1)
     dy = torch.randn_like(y)
-    ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask)
+    for algo in ("split", "fused"):
+        if algo == "fused" and mask is None:
+            continue
+        ops.attn_bwd(qkv, seg, y, dy, lse, B, T, H, H, hd, drop_seed=5, drop_p=0.1, drop_mask=mask, algo=algo)
 torch.cuda.synchronize()
 print("ok")

@@ -6,6 +6,7 @@
 #   bench [bench.py args]       one bench line                               -> gpurun_out/bench/
 #   prof  [tag] [bench args]    rocprofv3 --kernel-trace --stats of bench.py -> gpurun_out/prof_<tag>/
 #   attn  [tag]                 rocprofv3 --kernel-trace --stats of tools/attn_one.py -> gpurun_out/attn_<tag>/
+#   kprof <tag> <script> [args]  rocprofv3 --kernel-trace --stats of python <script> -> gpurun_out/kprof_<tag>/
 #   pmc   <tag> <script> "<counter set>" ["<counter set>" ...]
 #                               one rocprofv3 --pmc pass per counter set over python <script>
 #                                                                            -> gpurun_out/pmc_<tag>/
@@ -43,6 +44,13 @@ case "$cmd" in
     timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- \
       python tools/attn_one.py > $O/run.log 2>&1
     rc=$?; python tools/kstats.py $O/run_kernel_stats.csv 4 8; exit $rc ;;
+  kprof)
+    tag=$1; shift
+    O=gpurun_out/kprof_$tag
+    mkdir -p $O
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- \
+      python "$@" > $O/run.log 2>&1
+    rc=$?; tail -3 $O/run.log; exit $rc ;;
   pmc)
     tag=$1; script=$2; shift 2
     O=gpurun_out/pmc_$tag
