@@ -1197,9 +1197,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_mfma(const bf16_t* __res
 // attn_dq_finish_kernel (dq_acc -> the bf16 dqkv q columns, x scale, RoPE inverse, q-bias
 // partials).  Keep bits from the forward's words only (DROP 0 / 2).
 // ============================================================================
-#ifndef FB_DIAG
-#define FB_DIAG 0  // diagnostic builds only (results invalid): 1 phase B without its MFMAs, 2 no phase B
-#endif
 namespace fa {
 constexpr int FB_KEYS = 256;     // keys per block (8 waves x 32)
 constexpr int FB_DSB = 4 * IMG;  // one dS^T image set [256 keys][64 queries] bf16 (also the K image)
@@ -1275,19 +1272,21 @@ __device__ __forceinline__ float half_sum(float v) {
 }  // namespace fa
 
 // nd = -rowsum(dO o O) / dscale (the dP seed; delta of the FA2 preprocessing) and -lse * log2(e)
-// (the S seed), one row per (b, h, query): 8 lanes per row, 16-B loads of dO and O
+// (the S seed), one (b, query, head) per 8 lanes, 16-B loads of dO and O; consecutive groups take
+// consecutive heads of one token, so a wave reads whole token rows
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __restrict__ dy, long long lddy,
                                                             const bf16_t* __restrict__ yo, long long ldy,
                                                             const float* __restrict__ lse, float* __restrict__ nd,
                                                             float* __restrict__ nlse2, int T, int H, int hd,
                                                             float inv_dscale, long long nrows) {
-  const long long r = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const long long g = (long long)blockIdx.x * 32 + (threadIdx.x >> 3);  // (b T + q) H + h
   const int j = threadIdx.x & 7;
+  const long long row = g / H;                                          // b T + q
+  const int h = (int)(g - row * H);
+  const int b = (int)(row / T), q = (int)(row - (long long)b * T);
+  const long long r = ((long long)b * H + h) * T + q;                   // the [b][h][q] row index
   float s = 0.f;
-  if (r < nrows && 8 * j < hd) {
-    const long long bh = r / T;
-    const int q = (int)(r - bh * T), b = (int)(bh / H), h = (int)(bh - (long long)b * H);
-    const long long row = (long long)b * T + q;
+  if (g < nrows && 8 * j < hd) {
     const uint4 dv = *(const uint4*)(dy + row * lddy + (long long)h * hd + 8 * j);
     const uint4 ov = *(const uint4*)(yo + row * ldy + (long long)h * hd + 8 * j);
     const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w}, ow[4] = {ov.x, ov.y, ov.z, ov.w};
@@ -1300,7 +1299,7 @@ __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const bf16_t* __rest
   s += __shfl_xor(s, 1, 64);
   s += __shfl_xor(s, 2, 64);
   s += __shfl_xor(s, 4, 64);
-  if (r < nrows && j == 0) {
+  if (g < nrows && j == 0) {
     nd[r] = -s * inv_dscale;
     nlse2[r] = -lse[r] * 1.4426950408889634f;
   }
@@ -1372,285 +1371,128 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_mfma(const bf16_t* __re
     const int qe = window > 0 ? min(T, kb * FB_KEYS + FB_KEYS - 1 + window) : T;
     return (qe - 1) / KT;
   };
+  // the workgroup's whole sequence of (key block, query head, query tile) iterations: the LDS-DMA
+  // ring runs across the key-block seams, so a new block starts on landed data
+  const int h2_0 = kvh * rep;
   struct Cur {
-    int h2, qt;
+    int kb, h2, qt;
   };
+  auto next_of = [&](Cur cu) {
+    if (cu.qt < qt_end_of(cu.kb)) return Cur{cu.kb, cu.h2, cu.qt + 1};
+    if (cu.h2 + 1 < h2_0 + rep) return Cur{cu.kb, cu.h2 + 1, cu.kb * (FB_KEYS / KT)};
+    return Cur{cu.kb + 1, h2_0, (cu.kb + 1) * (FB_KEYS / KT)};
+  };
+  int total = 0;
+  for (int k = 0; k < nkb; ++k) total += (qt_end_of(k) - k * (FB_KEYS / KT) + 1) * rep;
   // the previous iteration's tile, finished (dQ) by waves 0-3 in the next iteration
   struct Prev {
-    int h2, qt, first, last;  // first / last key block that visits the tile
+    int h2, qt, first, last;  // the tile's first / last visiting key block is this one
   };
-  for (int kb = 0; kb < nkb; ++kb) {
-    const int kt0 = kb * FB_KEYS, kw0 = kt0 + wave * 32;
-    const int mykey = kw0 + (lane & 31);
-    const bool kok = mykey < T;
-    const bf16_t* krow = qkv + (rowbase + (kok ? mykey : 0)) * ld + koff;
-    const bf16_t* vrow = qkv + (rowbase + (kok ? mykey : 0)) * ld + voff;
-    v8bf kf[4], vf[4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      kf[ks] = scale_frag(frag_global(krow, kok, ks, hd, lane), c);
-      vf[ks] = frag_global(vrow, kok, ks, hd, lane);
-    }
-    // the lane's key bit in a pair-split word: key 2c -> bit c, key 2c+1 -> bit 16 + c
-    const uint32_t kpos = (uint32_t)(((mykey & 31) >> 1) + 16 * (mykey & 1));
-    v16f dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
-    float dscol = 0.f;  // (direct, bias) sum over the block's queries of dS/dscale for the lane's key
-    const int qt_begin = kt0 / KT, qt_end = qt_end_of(kb);
-    const int total = (qt_end - qt_begin + 1) * rep;
-    const int qt_end_prev = kb > 0 ? qt_end_of(kb - 1) : -1;  // tiles <= it were visited by block kb-1
-    const int mw_idx = kt0 / 32 + wave;  // this wave's key word of a query's keep bits
-    auto next_of = [&](Cur cu) { return cu.qt < qt_end ? Cur{cu.h2, cu.qt + 1} : Cur{cu.h2 + 1, qt_begin}; };
-    auto stage_dma = [&](Cur cu, int nb) {
-      const uint32_t buf = ring_l + nb * BUF;
-      piece_dma(buf, qsrc, cu.qt * qstride + (uint32_t)(cu.h2 * hd * 2), wave_u);
-      piece_dma(buf + IMG, dsrc, cu.qt * dstride + (uint32_t)(cu.h2 * hd * 2), wave_u);
-      const int q = cu.qt * KT + lane;
-      dma4(rrow, buf + row_lds, q < T ? (uint32_t)(((wave_u < 2 ? cu.h2 * T : 0) + q) * 4) : OORD);
-      if constexpr (DROP == 2)
-        dma4(rqm, buf + (uint32_t)(2 * IMG + 4 * 64 * 4 + wave_u * 64 * 4),
-             (q < T && mw_idx < wpr)
-                 ? (uint32_t)((((cu.h2 * (wpr >> 1) + (mw_idx >> 1)) * T + q) * 2 + (mw_idx & 1)) * 4)
-                 : OORD);
-    };
-    // the block's K image (rows kt0 .. kt0 + 255, unscaled) for the dQ product: 4 pieces per wave
+  auto stage_dma = [&](Cur cu, int nb) {
+    const uint32_t buf = ring_l + nb * BUF;
+    const int mw = cu.kb * (FB_KEYS / 32) + wave_u;  // this wave's key word of a query's keep bits
+    piece_dma(buf, qsrc, cu.qt * qstride + (uint32_t)(cu.h2 * hd * 2), wave_u);
+    piece_dma(buf + IMG, dsrc, cu.qt * dstride + (uint32_t)(cu.h2 * hd * 2), wave_u);
+    const int q = cu.qt * KT + lane;
+    dma4(rrow, buf + row_lds, q < T ? (uint32_t)(((wave_u < 2 ? cu.h2 * T : 0) + q) * 4) : OORD);
+    if constexpr (DROP == 2)
+      dma4(rqm, buf + (uint32_t)(2 * IMG + 4 * 64 * 4 + wave_u * 64 * 4),
+           (q < T && mw < wpr) ? (uint32_t)((((cu.h2 * (wpr >> 1) + (mw >> 1)) * T + q) * 2 + (mw & 1)) * 4)
+                               : OORD);
+  };
+  // a key block's K image (rows 256 kb .. + 255, unscaled) for the dQ product: 4 pieces per wave
+  auto kimg_dma = [&](int k) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      piece_dma(kimg_l + i * IMG, qsrc, (uint32_t)((kt0 + 64 * i) * ld * 2) + kcol, wave_u);
-    Cur cur{kvh * rep, qt_begin};
-    Cur n1 = next_of(cur);
-    Cur n2 = next_of(n1);
-    stage_dma(cur, 0);
-    if (total > 1) {
-      stage_dma(n1, 1);
-      dma_wait<NV>();
-    } else {
-      dma_wait<0>();
+      piece_dma(kimg_l + i * IMG, qsrc, (uint32_t)((k * FB_KEYS + 64 * i) * ld * 2) + kcol, wave_u);
+  };
+  // the lane's key of block k, and its K (x c) / V fragments
+  v8bf kf[4], vf[4];
+  auto load_kv = [&](int k) {
+    const int key = k * FB_KEYS + wave * 32 + (lane & 31);
+    const bool ok = key < T;
+    const bf16_t* krow = qkv + (rowbase + (ok ? key : 0)) * ld + koff;
+    const bf16_t* vrow = qkv + (rowbase + (ok ? key : 0)) * ld + voff;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      kf[ks] = scale_frag(frag_global(krow, ok, ks, hd, lane), c);
+      vf[ks] = frag_global(vrow, ok, ks, hd, lane);
     }
-    __syncthreads();
-    Prev pv{0, 0, 0, 0};
-    bool have_prev = false;
-    // waves 0-3: the dq_acc block of tile (h2, qt) this wave owns -- query half w >> 1, head dims
-    // 32 (w & 1) + acc_row(r): element r at + ((r & 3) + 8 (r >> 2)) * 32
-    auto dq_dst = [&](int h2, int qt) {
-      return dq_acc + dqa_off((long long)b * H + h2, nq32, qt * 2 + (wave_u >> 1), (wave_u & 1) * 32 + 4 * (lane >> 5)) +
-             (lane & 31);
-    };
-    // its old value, loaded at the end of the tile's own iteration (after the tile's phase A): the
-    // load latency runs under the barrier and the other waves' work instead of stalling phase B.
-    // Every wave loads on every iteration (waves 4-7 and first visits a line they ignore), so the
-    // registers are written on every path and no value of them lives through phase A.
-    v16f oldv;
-    // waves 0-3: dQ^T block of tile pv from the dS^T images, accumulated onto oldv.  Straight-line
-    // (inactive key waves wrote zero rows), operand reads one 4-k-step group ahead of the MFMAs
-    auto phase_b = [&](const char* dsimg, const Prev& p) __attribute__((always_inline)) {
-      const int qb = wave_u >> 1, cb = wave_u & 1;
-      const uint32_t ka0 = cb ? to.o[1][0] : to.o[0][0], ka1 = cb ? to.o[1][1] : to.o[0][1];
-      const uint32_t sb0 = qb ? to.o[1][0] : to.o[0][0], sb1 = qb ? to.o[1][1] : to.o[0][1];
-      float* dst = dq_dst(p.h2, p.qt);
-      v16f acc = p.first ? zero16() : oldv;  // the running sum, landed during the barrier
-      v8bf fa[2][4], fb[2][4];
-      auto rd = [&](int g) __attribute__((always_inline)) {
+  };
+  v16f dk0 = zero16(), dk1 = zero16(), dv0 = zero16(), dv1 = zero16();
+  float dscol = 0.f;  // (direct, bias) sum over the block's queries of dS/dscale for the lane's key
+  int kb = 0;
+  load_kv(0);
+  kimg_dma(0);
+  Cur cur{0, h2_0, 0};
+  Cur n1 = next_of(cur);
+  Cur n2 = next_of(n1);
+  stage_dma(cur, 0);
+  if (total > 1) {
+    stage_dma(n1, 1);
+    dma_wait<NV>();
+  } else {
+    dma_wait<0>();
+  }
+  __syncthreads();
+  Prev pv{0, 0, 0, 0};
+  bool have_prev = false;
+  // waves 0-3: the dq_acc block of tile (h2, qt) this wave owns -- query half w >> 1, head dims
+  // 32 (w & 1) + acc_row(r): element r at + ((r & 3) + 8 (r >> 2)) * 32
+  // (a wave-uniform base and a 32-bit lane offset: per-lane 64-bit pointers would be kept -- or
+  // spilled -- across the loop)
+  auto dq_base = [&](int h2, int qt) {
+    return dq_acc + dqa_off((long long)b * H + h2, nq32, qt * 2 + (wave_u >> 1), (wave_u & 1) * 32);
+  };
+  const uint32_t dq_lane = (uint32_t)(4 * (lane >> 5) * 32 + (lane & 31));
+  // its old value, loaded at the top of the tile's own iteration: the load latency runs under the
+  // tile's phase A instead of stalling phase B.  Every wave loads on every iteration (waves 4-7 and
+  // first visits a line they ignore), so the registers are written on every path.
+  v16f oldv;
+  // waves 0-3: dQ^T block of tile pv from the dS^T images, accumulated onto oldv.  Straight-line
+  // (inactive key waves wrote zero rows), operand reads one 4-k-step group ahead of the MFMAs
+  auto phase_b = [&](const char* dsimg, const Prev& p) __attribute__((always_inline)) {
+    const int qb = wave_u >> 1, cb = wave_u & 1;
+    const uint32_t ka0 = cb ? to.o[1][0] : to.o[0][0], ka1 = cb ? to.o[1][1] : to.o[0][1];
+    const uint32_t sb0 = qb ? to.o[1][0] : to.o[0][0], sb1 = qb ? to.o[1][1] : to.o[0][1];
+    float* dst = dq_base(p.h2, p.qt);
+    v16f acc = p.first ? zero16() : oldv;  // the running sum, landed under the previous phase A
+    v8bf fa[2][4], fb[2][4];
+    auto rd = [&](int g) __attribute__((always_inline)) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kk = 4 * g + i, rb = 32 * ((kk >> 1) & 1), st = kk & 1;
-          fa[g & 1][i] = frag_tr_p(kimg + g * IMG, ka0, ka1, rb, st);
-          fb[g & 1][i] = frag_tr_p(dsimg + g * IMG, sb0, sb1, rb, st);
-        }
-      };
-      rd(0);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (g < 3) rd(g + 1);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (FB_DIAG != 1) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[g & 1][i], fb[g & 1][i], acc, 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (!p.last || !direct) {  // a later key block adds to it (or the finish pass converts it)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) dst[((r & 3) + 8 * (r >> 2)) * 32] = acc[r];
-      } else if (cb * 32 < hd) {  // the tile's last key block: dQ = qscale (dS/dscale . K) into dqkv
-        const int q = p.qt * KT + qb * 32 + (lane & 31);
-        const bool qok = q < T;
-        bf16_t* drow = dqkv + (rowbase + (qok ? q : 0)) * lddq + (long long)p.h2 * hd + cb * 32;
-        store_blk16(drow, acc, qscale, qok, hd - cb * 32 < 32 ? hd - cb * 32 : 32, lane);
+      for (int i = 0; i < 4; ++i) {
+        const int kk = 4 * g + i, rb = 32 * ((kk >> 1) & 1), st = kk & 1;
+        fa[g & 1][i] = frag_tr_p(kimg + g * IMG, ka0, ka1, rb, st);
+        fb[g & 1][i] = frag_tr_p(dsimg + g * IMG, sb0, sb1, rb, st);
       }
     };
-    // one iteration on ring buffer CUR (compile-time: every image read is lane offset + immediate)
-    auto iter = [&](auto cur_c, int it) __attribute__((always_inline)) {
-      constexpr int CUR = decltype(cur_c)::value;
-      const char* buf = smem + CUR * BUF;
-      const char* Qi = buf;
-      const char* Di = buf + IMG;
-      const float* lse2s = (const float*)(buf + 2 * IMG);
-      const float* nds = lse2s + 64;
-      const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
-      const uint32_t* mws = (const uint32_t*)(buf + 2 * IMG + 4 * 64 * 4) + wave * 64;
-      // the dS^T store offsets are rebuilt each iteration from (sbase, sg), which the empty asm makes
-      // opaque: hoisted out of the loop, the eight per-lane offsets would stay live through phase A
-      uint32_t sb_i = sbase;
-      int sg_i = sg;
-      asm volatile("" : "+v"(sb_i), "+v"(sg_i));
-      char* dsw = dsb + (it & 1) * FB_DSB + sb_i;
-      const bool more1 = it + 1 < total, more2 = it + 2 < total;
-      // the previous tile's dQ first: its dq_acc loads and stores precede this iteration's DMAs in
-      // vmcnt order, so the counted waits below leave exactly the newest stage in flight
-      if (FB_DIAG != 2 && wave_u < 4 && have_prev) phase_b(dsb + ((it - 1) & 1) * FB_DSB, pv);
+    rd(0);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if (g < 3) rd(g + 1);
       __builtin_amdgcn_sched_barrier(0);
-      if (more2) stage_dma(n2, (CUR + 2) % 3);  // that buffer was last read before the previous barrier
-      const int q0 = cur.qt * KT;
-      const int qlast = min(T - 1, q0 + KT - 1);
-      auto lo_at = [&](int i) { return window > 0 ? max(los[i], q0 + i - window + 1) : los[i]; };
-      const int lo0 = lo_at(0);
-      // wave activity: some query of the tile sees some key of the wave (lo is monotone in q)
-      const bool active = (qlast >= kt0 + 32 * wave_u) && (lo0 <= kt0 + 32 * wave_u + 31);
-      auto phase_sdp = [&](int qb, v16f& s, v16f& dp, v16f& nd) __attribute__((always_inline)) {
 #pragma unroll
-        for (int rg = 0; rg < 16; rg += 4) {
-          const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
-          nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
-          const float4 l4 = *(const float4*)(lse2s + qb * 32 + acc_row(rg, lane));
-          s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
-        }
-        dp = nd;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks) {
-          if (ks < nks) {
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Qi, ro, qb * 32, ks), kf[ks], s, 0, 0, 0);
-            dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
-          }
-        }
-      };
-      auto phase_ds = [&](int qb, auto full_c, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1,
-                          v8bf& sb0, v8bf& sb1) __attribute__((always_inline)) {
-        bool full;
-        if constexpr (std::is_same_v<decltype(full_c), bool>) full = full_c;
-        else full = decltype(full_c)::value;
-        if (!full) {
-#pragma unroll
-          for (int rg = 0; rg < 16; rg += 4) {
-            const int qi = qb * 32 + acc_row(rg, lane);
-            const int4 lo4 = *(const int4*)(los + qi);
-            const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const int q = q0 + qi + u;
-              const int lq = window > 0 ? max(lov[u], q - window + 1) : lov[u];
-              s[rg + u] = ((mykey > q) | (mykey < lq) | (q >= T)) ? -INFINITY : s[rg + u];
-            }
-          }
-        }
-        v16f pd;
-#pragma unroll
-        for (int rg = 0; rg < 16; rg += 4) {
-          const int qi = qb * 32 + acc_row(rg, lane);
-          uint4 mw4 = make_uint4(0, 0, 0, 0);
-          if constexpr (DROP == 2) mw4 = *(const uint4*)(mws + qi);
-          const uint32_t mwv[4] = {mw4.x, mw4.y, mw4.z, mw4.w};
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int r = rg + u;
-            const float p = __builtin_amdgcn_exp2f(s[r]);
-            float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
-            if constexpr (DROP == 2) {
-              const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
-              pdr = __uint_as_float(__float_as_uint(p) & m);
-              s[r] = p * bsel(m, dp[r], nd[r]);
-            } else {
-              s[r] = p * dp[r];
-            }
-            pd[r] = pdr;
-          }
-        }
-        pb0 = pack_b(pd, 0); pb1 = pack_b(pd, 1);
-        sb0 = pack_b(s, 0); sb1 = pack_b(s, 1);
-      };
-      struct TrFr { v8bf d[4], q[4]; };
-      auto tr_frags = [&](int qb, TrFr& f) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < (hd > 32 ? 4 : 2); ++i) {
-          f.d[i] = frag_tr_o(Di, to, qb * 32, i & 1, i >> 1);
-          f.q[i] = frag_tr_o(Qi, to, qb * 32, i & 1, i >> 1);
-        }
-      };
-      auto phase_dkdv = [&](const TrFr& f, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
-                            __attribute__((always_inline)) {
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[0], pb0, dv0, 0, 0, 0);
-        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[1], pb1, dv0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[0], sb0, dk0, 0, 0, 0);
-        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[1], sb1, dk0, 0, 0, 0);
-        if constexpr (hd > 32) {
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[2], pb0, dv1, 0, 0, 0);
-          dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[3], pb1, dv1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[2], sb0, dk1, 0, 0, 0);
-          dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[3], sb1, dk1, 0, 0, 0);
-        }
-      };
-      auto body = [&](auto full) __attribute__((always_inline)) {
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-          v16f s, dp, nd;
-          v8bf x0, x1, x2, x3;
-          TrFr f;
-          phase_sdp(qb, s, dp, nd);
-          tr_frags(qb, f);
-          __builtin_amdgcn_sched_barrier(0);
-          phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
-          if (direct && bpart) {
-            float t = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) t += s[r];
-            dscol += t;
-          }
-          // dS^T rows of this wave's keys: x2 = queries 4h + {0..3, 8..11}, x3 = 4h + {16..19, 24..27}
-          // of the half, i.e. chunks 4 qb + 0..3 of the image row, 8 bytes at 8 (lane >> 5) in each
-          const v4u_a w0 = __builtin_bit_cast(v4u_a, x2), w1 = __builtin_bit_cast(v4u_a, x3);
-          *(uint2*)(dsw + 16 * ((4 * qb + 0) ^ sg_i)) = make_uint2(w0[0], w0[1]);
-          *(uint2*)(dsw + 16 * ((4 * qb + 1) ^ sg_i)) = make_uint2(w0[2], w0[3]);
-          *(uint2*)(dsw + 16 * ((4 * qb + 2) ^ sg_i)) = make_uint2(w1[0], w1[1]);
-          *(uint2*)(dsw + 16 * ((4 * qb + 3) ^ sg_i)) = make_uint2(w1[2], w1[3]);
-          phase_dkdv(f, x0, x1, x2, x3);
-        }
-      };
-      if (active) {
-        const bool full = (q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0);
-        body(full);
-      } else {  // no visible pair: zero dS^T rows, so the dQ product runs straight through
-#pragma unroll
-        for (int c8 = 0; c8 < 8; ++c8) *(uint2*)(dsw + 16 * (c8 ^ sg_i)) = make_uint2(0u, 0u);
-      }
-      pv = Prev{cur.h2, cur.qt, cur.qt > qt_end_prev ? 1 : 0, (cur.qt >> 2) == kb ? 1 : 0};
-      have_prev = true;
-      __builtin_amdgcn_sched_barrier(0);  // keep the loads (and their 16 registers) out of phase A
-      {
-        const float* src = wave_u < 4 ? dq_dst(cur.h2, cur.qt) : dq_acc + (lane & 31);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) oldv[r] = src[((r & 3) + 8 * (r >> 2)) * 32];
-      }
-      // n1's data (issued an iteration ago) landed; n2's DMAs -- and the 16 oldv loads issued after
-      // them -- may still be in flight
-      if (more1) {
-        if (more2) dma_wait<NV + 16>();
-        else dma_wait<16>();
-      }
-      cur = n1;
-      n1 = n2;
-      n2 = next_of(n2);
-      // raw barrier: no vmcnt(0) (n2's DMAs stay in flight); the dS^T stores and this wave's image
-      // reads retired first
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-    for (int it = 0; it < total; it += 3) {
-      iter(std::integral_constant<int, 0>{}, it);
-      if (it + 1 < total) iter(std::integral_constant<int, 1>{}, it + 1);
-      if (it + 2 < total) iter(std::integral_constant<int, 2>{}, it + 2);
+      for (int i = 0; i < 4; ++i)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[g & 1][i], fb[g & 1][i], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (wave_u < 4) phase_b(dsb + ((total - 1) & 1) * FB_DSB, pv);  // the last tile's dQ
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the block
-    __syncthreads();  // the K / dS^T images are free (bias scratch, the next block's K image)
+    if (!p.last || !direct) {  // a later key block adds to it (or the finish pass converts it)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dst[dq_lane + ((r & 3) + 8 * (r >> 2)) * 32] = acc[r];
+    } else if (cb * 32 < hd) {  // the tile's last key block: dQ = qscale (dS/dscale . K) into dqkv
+      const int q0b = p.qt * KT + qb * 32;
+      const bool qok = q0b + (lane & 31) < T;
+      bf16_t* dbase = dqkv + (rowbase + q0b) * lddq + (long long)p.h2 * hd + cb * 32;
+      store_blk16(dbase + (uint32_t)(qok ? (lane & 31) * (uint32_t)lddq : 0u), acc, qscale, qok,
+                  hd - cb * 32 < 32 ? hd - cb * 32 : 32, lane);
+    }
+  };
+  // end of key block k (its last tile's dQ done, every wave past the barrier that follows it): dK,
+  // dV (and, direct, the q-bias partial) out; the bias column sums use the dS^T / K image region
+  // (the ring may hold the next block's first tiles in flight)
+  auto block_epilogue = [&](int k) __attribute__((always_inline)) {
+    const int mykey = k * FB_KEYS + wave * 32 + (lane & 31);
+    const bool kok = mykey < T;
     if (rcos) {  // RoPE: dK w.r.t. the rotated k, rotated back at the key's position
       const size_t ro2 = (size_t)(kok ? mykey : 0) * (hd / 2);
       rope_inv_blocks<hd>(dk0, dk1, rcos + ro2, rsin + ro2, lane >> 5);
@@ -1665,17 +1507,18 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_mfma(const bf16_t* __re
         store_blk16(vr + 32, dv1, vsc, kok, hd - 32, lane);
       }
     }
-    if (bpart) {  // k / v (and q) bias partials of the block into row 2 kb of the batch's 128-row tiles
-      float* red = (float*)smem;
-      const float vk = colsum_wg8(dk0, dk1, kscale, kok, red, wave, lane, tid);
-      const float vv = colsum_wg8(dv0, dv1, vsc, kok, red, wave, lane, tid);
-      float vq = 0.f;
-      if (direct) {  // sum_key dscol[key] K[key][d], K from the block's image (raw bf16)
+    if (bpart) {  // k / v (and q) bias partials of the block into row 2 k of the batch's 128-row tiles
+      float* red = (float*)dsb;
+      v16f x0, x1;
+      if (direct) {  // sum_key dscol[key] K[key][d], K from the block's image (raw bf16) -- read
+        // before the column sums write over it (COLSUM8_LDS reaches into the K image)
         uint32_t kr_o = (uint32_t)((wave >> 1) * IMG + srow * 128 + 8 * (lane >> 5));
         int sg_k = sg;
-        asm volatile("" : "+v"(kr_o), "+v"(sg_k));  // (not hoisted out of the key-block loop)
+        asm volatile("" : "+v"(kr_o), "+v"(sg_k));  // (not hoisted out of the iteration loop)
         const char* krow_l = kimg + kr_o;
-        v16f x0, x1;
+        // lanes l and l + 32 hold the same key's two halves of the query rows: the whole column sum
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dscol), __float_as_uint(dscol), false, false);
+        const float dsall = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1685,24 +1528,216 @@ __global__ __launch_bounds__(512, 2) void attn_bwd_fused_mfma(const bf16_t* __re
             const float k4[4] = {__uint_as_float(kv.x << 16), __uint_as_float(kv.x & 0xFFFF0000u),
                                  __uint_as_float(kv.y << 16), __uint_as_float(kv.y & 0xFFFF0000u)};
 #pragma unroll
-            for (int t = 0; t < 4; ++t) (cbk ? x1 : x0)[4 * j + t] = dscol * k4[t];
+            for (int t = 0; t < 4; ++t) (cbk ? x1 : x0)[4 * j + t] = dsall * k4[t];
           }
-        vq = colsum_wg8(x0, x1, qscale, kok, red, wave, lane, tid);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __syncthreads();  // every wave's K row read before the first column sum writes over it
       }
-      float* dst = bpart + ((long long)b * ny + 2 * kb) * ldp;
+      const float vk = colsum_wg8(dk0, dk1, kscale, kok, red, wave, lane, tid);
+      const float vv = colsum_wg8(dv0, dv1, vsc, kok, red, wave, lane, tid);
+      const float vq = direct ? colsum_wg8(x0, x1, qscale, kok, red, wave, lane, tid) : 0.f;
+      float* dst = bpart + ((long long)b * ny + 2 * k) * ldp;
       const long long qoff = (long long)kvh * hd;  // (direct: rep == 1, the query head is kvh)
       if (tid < hd) {
         dst[koff + tid] = vk;
         dst[voff + tid] = vv;
         if (direct) dst[qoff + tid] = vq;
-        if (2 * kb + 1 < ny) {  // the block's second 128-row tile: its sums are in row 2 kb
+        if (2 * k + 1 < ny) {  // the block's second 128-row tile: its sums are in row 2 k
           dst[ldp + koff + tid] = 0.f;
           dst[ldp + voff + tid] = 0.f;
           if (direct) dst[ldp + qoff + tid] = 0.f;
         }
       }
     }
+  };
+  // one iteration on ring buffer CUR (compile-time: every image read is lane offset + immediate)
+  auto iter = [&](auto cur_c, int it) __attribute__((always_inline)) {
+    constexpr int CUR = decltype(cur_c)::value;
+    const char* buf = smem + CUR * BUF;
+    const char* Qi = buf;
+    const char* Di = buf + IMG;
+    const float* lse2s = (const float*)(buf + 2 * IMG);
+    const float* nds = lse2s + 64;
+    const int* los = (const int*)(buf + 2 * IMG + 2 * 64 * 4);
+    const uint32_t* mws = (const uint32_t*)(buf + 2 * IMG + 4 * 64 * 4) + wave * 64;
+    const int kt0 = kb * FB_KEYS, kw0 = kt0 + wave * 32;
+    const int mykey = kw0 + (lane & 31);
+    // the lane's key bit in a pair-split word: key 2c -> bit c, key 2c+1 -> bit 16 + c
+    const uint32_t kpos = (uint32_t)(((mykey & 31) >> 1) + 16 * (mykey & 1));
+    // the dS^T store offsets are rebuilt each iteration from (sbase, sg), which the empty asm makes
+    // opaque: hoisted out of the loop, the eight per-lane offsets would stay live through phase A
+    uint32_t sb_i = sbase;
+    int sg_i = sg;
+    asm volatile("" : "+v"(sb_i), "+v"(sg_i));
+    char* dsw = dsb + (it & 1) * FB_DSB + sb_i;
+    const bool more1 = it + 1 < total, more2 = it + 2 < total;
+    // the previous tile's dQ first: its stores precede this iteration's DMAs in vmcnt order, so the
+    // counted waits below leave exactly the newest stage (and the oldv loads) in flight
+    if (wave_u < 4 && have_prev) phase_b(dsb + ((it - 1) & 1) * FB_DSB, pv);
+    __builtin_amdgcn_sched_barrier(0);
+    if (more2) stage_dma(n2, (CUR + 2) % 3);  // that buffer was last read before the previous barrier
+    {  // this tile's dq_acc value for its phase B in the next iteration: in flight under phase A
+      const float* src = wave_u < 4 ? dq_base(cur.h2, cur.qt) : dq_acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oldv[r] = src[dq_lane + ((r & 3) + 8 * (r >> 2)) * 32];
+    }
+    const int q0 = cur.qt * KT;
+    const int qlast = min(T - 1, q0 + KT - 1);
+    auto lo_at = [&](int i) { return window > 0 ? max(los[i], q0 + i - window + 1) : los[i]; };
+    const int lo0 = lo_at(0);
+    // wave activity: some query of the tile sees some key of the wave (lo is monotone in q)
+    const bool active = (qlast >= kt0 + 32 * wave_u) && (lo0 <= kt0 + 32 * wave_u + 31);
+    auto phase_sdp = [&](int qb, v16f& s, v16f& dp, v16f& nd) __attribute__((always_inline)) {
+#pragma unroll
+      for (int rg = 0; rg < 16; rg += 4) {
+        const float4 n4 = *(const float4*)(nds + qb * 32 + acc_row(rg, lane));
+        nd[rg] = n4.x; nd[rg + 1] = n4.y; nd[rg + 2] = n4.z; nd[rg + 3] = n4.w;
+        const float4 l4 = *(const float4*)(lse2s + qb * 32 + acc_row(rg, lane));
+        s[rg] = l4.x; s[rg + 1] = l4.y; s[rg + 2] = l4.z; s[rg + 3] = l4.w;
+      }
+      dp = nd;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        if (ks < nks) {
+          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Qi, ro, qb * 32, ks), kf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag_row_o(Di, ro, qb * 32, ks), vf[ks], dp, 0, 0, 0);
+        }
+      }
+    };
+    auto phase_ds = [&](int qb, auto full_c, v16f& s, const v16f& dp, const v16f& nd, v8bf& pb0, v8bf& pb1,
+                        v8bf& sb0, v8bf& sb1) __attribute__((always_inline)) {
+      bool full;
+      if constexpr (std::is_same_v<decltype(full_c), bool>) full = full_c;
+      else full = decltype(full_c)::value;
+      if (!full) {
+#pragma unroll
+        for (int rg = 0; rg < 16; rg += 4) {
+          const int qi = qb * 32 + acc_row(rg, lane);
+          const int4 lo4 = *(const int4*)(los + qi);
+          const int lov[4] = {lo4.x, lo4.y, lo4.z, lo4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int q = q0 + qi + u;
+            const int lq = window > 0 ? max(lov[u], q - window + 1) : lov[u];
+            s[rg + u] = ((mykey > q) | (mykey < lq) | (q >= T)) ? -INFINITY : s[rg + u];
+          }
+        }
+      }
+      v16f pd;
+#pragma unroll
+      for (int rg = 0; rg < 16; rg += 4) {
+        const int qi = qb * 32 + acc_row(rg, lane);
+        uint4 mw4 = make_uint4(0, 0, 0, 0);
+        if constexpr (DROP == 2) mw4 = *(const uint4*)(mws + qi);
+        const uint32_t mwv[4] = {mw4.x, mw4.y, mw4.z, mw4.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = rg + u;
+          const float p = __builtin_amdgcn_exp2f(s[r]);
+          float pdr = p;  // the 1/(1-p) of P~ is applied to dV once at the end
+          if constexpr (DROP == 2) {
+            const uint32_t m = (uint32_t)keep_mask(mwv[u], kpos);
+            pdr = __uint_as_float(__float_as_uint(p) & m);
+            s[r] = p * bsel(m, dp[r], nd[r]);
+          } else {
+            s[r] = p * dp[r];
+          }
+          pd[r] = pdr;
+        }
+      }
+      pb0 = pack_b(pd, 0); pb1 = pack_b(pd, 1);
+      sb0 = pack_b(s, 0); sb1 = pack_b(s, 1);
+    };
+    struct TrFr { v8bf d[4], q[4]; };
+    auto tr_frags = [&](int qb, TrFr& f) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < (hd > 32 ? 4 : 2); ++i) {
+        f.d[i] = frag_tr_o(Di, to, qb * 32, i & 1, i >> 1);
+        f.q[i] = frag_tr_o(Qi, to, qb * 32, i & 1, i >> 1);
+      }
+    };
+    auto phase_dkdv = [&](const TrFr& f, const v8bf& pb0, const v8bf& pb1, const v8bf& sb0, const v8bf& sb1)
+                          __attribute__((always_inline)) {
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[0], pb0, dv0, 0, 0, 0);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[1], pb1, dv0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[0], sb0, dk0, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[1], sb1, dk0, 0, 0, 0);
+      if constexpr (hd > 32) {
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[2], pb0, dv1, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.d[3], pb1, dv1, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[2], sb0, dk1, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.q[3], sb1, dk1, 0, 0, 0);
+      }
+    };
+    auto body = [&](auto full) __attribute__((always_inline)) {
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        v16f s, dp, nd;
+        v8bf x0, x1, x2, x3;
+        TrFr f;
+        phase_sdp(qb, s, dp, nd);
+        phase_ds(qb, full, s, dp, nd, x0, x1, x2, x3);
+        tr_frags(qb, f);  // (after the VALU: the registers hold oldv through phase A)
+        if (direct && bpart) {
+          float t = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) t += s[r];
+          dscol += t;
+        }
+        // dS^T rows of this wave's keys: x2 = queries 4h + {0..3, 8..11}, x3 = 4h + {16..19, 24..27}
+        // of the half, i.e. chunks 4 qb + 0..3 of the image row, 8 bytes at 8 (lane >> 5) in each
+        const v4u_a w0 = __builtin_bit_cast(v4u_a, x2), w1 = __builtin_bit_cast(v4u_a, x3);
+        *(uint2*)(dsw + 16 * ((4 * qb + 0) ^ sg_i)) = make_uint2(w0[0], w0[1]);
+        *(uint2*)(dsw + 16 * ((4 * qb + 1) ^ sg_i)) = make_uint2(w0[2], w0[3]);
+        *(uint2*)(dsw + 16 * ((4 * qb + 2) ^ sg_i)) = make_uint2(w1[0], w1[1]);
+        *(uint2*)(dsw + 16 * ((4 * qb + 3) ^ sg_i)) = make_uint2(w1[2], w1[3]);
+        phase_dkdv(f, x0, x1, x2, x3);
+      }
+    };
+    if (active) {
+      const bool full = (q0 >= kw0 + 31) && (q0 + KT - 1 < T) && (lo_at(qlast - q0) <= kw0);
+      body(full);
+    } else {  // no visible pair: zero dS^T rows, so the dQ product runs straight through
+#pragma unroll
+      for (int c8 = 0; c8 < 8; ++c8) *(uint2*)(dsw + 16 * (c8 ^ sg_i)) = make_uint2(0u, 0u);
+    }
+    pv = Prev{cur.h2, cur.qt, (kb == 0 || cur.qt > qt_end_of(kb - 1)) ? 1 : 0, (cur.qt >> 2) == kb ? 1 : 0};
+    have_prev = true;
+    // n1's data (issued an iteration ago) landed; n2's DMAs -- and the 16 oldv loads issued after
+    // them -- may still be in flight
+    if (more1) {
+      if (more2) dma_wait<NV + 16>();
+      else dma_wait<16>();
+    }
+    cur = n1;
+    n1 = n2;
+    n2 = next_of(n2);
+    // raw barrier: no vmcnt(0) (n2's DMAs stay in flight); the dS^T stores and this wave's image
+    // reads retired first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (more1 && cur.kb != kb) {  // key-block seam (the next tile's data already landed)
+      load_kv(cur.kb);            // the new block's fragments, in flight under the epilogue
+      if (wave_u < 4) phase_b(dsb + (it & 1) * FB_DSB, pv);  // the finished block's last tile
+      __syncthreads();            // its dS^T / K images are free
+      block_epilogue(kb);
+      dk0 = zero16(); dk1 = zero16(); dv0 = zero16(); dv1 = zero16();
+      dscol = 0.f;
+      kimg_dma(cur.kb);           // lands before the new block's first phase B (two waits ahead)
+      kb = cur.kb;
+      have_prev = false;
+    }
+  };
+  for (int it = 0; it < total; it += 3) {
+    iter(std::integral_constant<int, 0>{}, it);
+    if (it + 1 < total) iter(std::integral_constant<int, 1>{}, it + 1);
+    if (it + 2 < total) iter(std::integral_constant<int, 2>{}, it + 2);
   }
+  if (wave_u < 4) phase_b(dsb + ((total - 1) & 1) * FB_DSB, pv);  // the last tile's dQ
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing in flight past the loop
+  __syncthreads();
+  block_epilogue(kb);
 }
 
 // dq_acc (fp32 sums of dS/dscale . K over all keys, fa::dqa_off layout) -> the bf16 dqkv q columns:

@@ -742,25 +742,42 @@ int aux_backward(const Ctx& C, int accumulate) {
   const int d = D.d;
   const long long M = C.M;
   const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
+  // the offset heads' two d x d weight gradients each -- and the termination head's -- (bf16: one
+  // grouped launch after the loop, as the blocks' dW; their dY operands stay in per-head buffers)
+  cg_dw_group grp;
+  memset(&grp, 0, sizeof(grp));
+  grp.K = (int)M;
+  grp.tile_m = 128;  // 10 products of d x d at C5: the 128-row tile gives the most workgroups
   if (m->cfg.termination_aux) {
     const int nc = m->cfg.termination_n_classes, ncp = (int)rup(nc, 16);
     if (m->d_term_logits) {
       if (!m->aux_ready || m->ld_d_term < nc) return CG_EINVAL;
       CK(cg_cast_pad_2d(m->d_term_logits, m->ld_d_term, (int)M, nc, C.dt, A.dlogits, ncp, ncp, C.s));
-      // dW_t = dT^T . xf over the padded rows (pad rows of dT^T are zero)
-      cg_gemm_desc g = gdesc(C);
-      g.c_dtype = CG_F32;
-      g.M = ncp; g.N = d; g.K = (int)M;
-      g.A = A.dlogits; g.lda = ncp; g.a_kcontig = 0;
-      g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
-      g.C = G(C, C.Lo.termw); g.ldc = d;
-      g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
-      g.split_k = pick_split(C, ncp, d, M);
-      g.workspace = A.splitws;
-      g.ws_bytes = A.nb.splitws;
-      CK(cg_gemm(&g, C.s));
+      // dW_t = dT^T . xf over the padded rows (pad rows of dT^T are zero): bf16 in the grouped launch
+      // (A.dlogits is not written again before it), fp32 as its own split-K product
+      if (C.dt == CG_BF16) {
+        cg_dw_product& q = grp.p[grp.n++];
+        q.A = A.dlogits; q.lda = ncp;
+        q.B = A.xf; q.ldb = d;
+        q.C = G(C, C.Lo.termw); q.ldc = d;
+        q.N_out = ncp; q.K_out = d;
+        q.alpha = 1.0f; q.accumulate = accumulate;
+      } else {
+        cg_gemm_desc g = gdesc(C);
+        g.c_dtype = CG_F32;
+        g.M = ncp; g.N = d; g.K = (int)M;
+        g.A = A.dlogits; g.lda = ncp; g.a_kcontig = 0;
+        g.B = A.xf; g.ldb = d; g.b_kcontig = 0;
+        g.C = G(C, C.Lo.termw); g.ldc = d;
+        g.epilogue = accumulate ? CG_EPI_ACCUM : 0;
+        g.split_k = pick_split(C, ncp, d, M);
+        g.workspace = A.splitws;
+        g.ws_bytes = A.nb.splitws;
+        CK(cg_gemm(&g, C.s));
+      }
       CK(cg_colsum(CG_F32, m->d_term_logits, m->ld_d_term, (int)M, nc, G(C, C.Lo.termb), accumulate, A.colws,
                    A.nb.colws, C.s));
+      cg_gemm_desc g = gdesc(C);
       // dxf += dT . W_t
       g = lin_dx(C, A.dlogits, ncp, C.Lo.termw, d, ncp, d, A.dtmp, d);
       g.c_dtype = CG_F32;
@@ -772,12 +789,6 @@ int aux_backward(const Ctx& C, int accumulate) {
     }
   }
   const int noff = std::min(m->cfg.n_offsets, 8);
-  // the offset heads' two d x d weight gradients each (bf16: one grouped launch after the loop,
-  // as the blocks' dW; their dY operands stay in per-head buffers)
-  cg_dw_group grp;
-  memset(&grp, 0, sizeof(grp));
-  grp.K = (int)M;
-  grp.tile_m = 128;  // 10 products of d x d at C5: the 128-row tile gives the most workgroups
   auto add_dw = [&](const void* dy, const void* x, long long goff) -> int {
     if (C.dt != CG_BF16) return lin_dw(C, dy, d, x, d, d, d, goff, d, accumulate);
     cg_dw_product& q = grp.p[grp.n++];
@@ -1024,10 +1035,15 @@ extern "C" int cg_model_aux_forward(cg_model* m, float* term_logits, long long l
   const Acts& A = C.A;
   const int d = D.d;
   if (nc > 0) {
-    cg_gemm_desc g = lin_fwd(C, A.xf, d, C.Lo.termw, d, nc, d, term_logits, ld_term);
+    // N padded to the weight's 16 zero-padded rows (an extent the MFMA tiles take; the bias reads of
+    // the pad columns stay inside the bias's 256-B aligned slot), then the nc columns copied out.
+    // A.dtmp is backward scratch, free until the backward's head products
+    const int ncp = (int)rup(nc, 16);
+    cg_gemm_desc g = lin_fwd(C, A.xf, d, C.Lo.termw, d, ncp, d, A.dtmp, ncp);
     g.c_dtype = CG_F32;
     g.epilogue = CG_EPI_BIAS; g.bias = P(C, C.Lo.termb);
     CK(cg_gemm(&g, C.s));
+    CK(cg_cast_pad_2d(A.dtmp, ncp, (int)C.M, nc, CG_F32, term_logits, ld_term, nc, C.s));
   }
   const long long hoff = m->cfg.tie_embeddings ? C.Lo.tok : C.Lo.head;
   for (int i = 0; i < noff; ++i) {
