@@ -71,7 +71,7 @@ def flops_per_token(c, V=68):
 
 
 def probe_pass(kind, run, first, n):
-    """Run n untimed steps with the live probe on `kind`; returns (work, ms, launches)."""
+    """Run n untimed steps with the live probe on `kind`; returns (work, ms, launches, bytes)."""
     import ctypes as C
     from codonlm_amd import _lib as L
     L.lib.cg_probe_enable(kind)
@@ -80,8 +80,10 @@ def probe_pass(kind, run, first, n):
     torch.cuda.synchronize()
     w, ms, k = C.c_double(0), C.c_double(0), C.c_longlong(0)
     L.check(L.lib.cg_probe_read(C.byref(w), C.byref(ms), C.byref(k)), "cg_probe_read")
+    nbytes = C.c_double(0)
+    L.check(L.lib.cg_probe_bytes(C.byref(nbytes)), "cg_probe_bytes")
     L.lib.cg_probe_enable(0)
-    return w.value, ms.value, k.value
+    return w.value, ms.value, k.value, nbytes.value
 
 
 def _cpu_share():
@@ -166,6 +168,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-roofline", action="store_true")
+    ap.add_argument("--attn-bwd", default="auto", choices=["auto", "split", "fused"],
+                    help="bf16 attention backward (cg_model_opts.attn_bwd_algo; A/B runs, default automatic)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -188,7 +192,8 @@ def main():
     model = TinyGPT(68, T, n_layer=c["n_layer"], n_head=c["n_head"], n_embd=c["n_embd"], dropout=0.1,
                     label_smoothing=0.05, n_kv_head=c["kv"], use_swiglu=c["swiglu"], use_rope=c["rope"],
                     termination_aux=bool(c.get("term")), multi_offset_targets=list(c.get("offsets", ())) or None,
-                    compute_dtype=args.dtype, device=dev)
+                    compute_dtype=args.dtype, device=dev,
+                    engine_opts={"attn_bwd_algo": {"auto": 0, "split": 1, "fused": 2}[args.attn_bwd]})
     if world > 1:  # identical replicas
         dist.broadcast(model.flat_parameters(), 0)
     model.train()
@@ -285,7 +290,7 @@ def main():
     if not args.no_kernel_roofline and args.dtype == "bf16":
         nxt = args.warmup
         for kind in (L.PROBE_GEMM_PERS, L.PROBE_GEMM_DW_GROUPED, L.PROBE_GEMM_DW, L.PROBE_GEMM_FWD, L.PROBE_GEMM_DX,
-                     L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV):
+                     L.PROBE_ATTN_FWD, L.PROBE_ATTN_DQ, L.PROBE_ATTN_DKDV, L.PROBE_ATTN_BWD, L.PROBE_DW_SLAB):
             probes[kind] = probe_pass(kind, run, nxt, 2)
             nxt += 2
         # the roofline kernel is the MFMA kernel class with the most device time per step (a class =
@@ -364,7 +369,8 @@ def main():
                    "model": "TinyGPT (genomics-lm src/codonlm)", "global_batch": world * B, "seq_len": T,
                    "micro_batch_per_gpu": B, "parallelism": f"dp{world}", "dropout": 0.1,
                    "label_smoothing": 0.05, "sep_mask": True,
-                   "path": args.path if (not aux or fwd_only) else "trainer"},
+                   "path": args.path if (not aux or fwd_only) else "trainer",
+                   **({"attn_bwd": args.attn_bwd} if args.attn_bwd != "auto" else {})},
         "final_loss": round(final_loss, 4),
         "model_flops_per_token": ftok,
         "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),
@@ -403,11 +409,21 @@ def main():
                                                     f"(collected at {t.get('commit')}; this run {_head()})")
             result["roofline"]["traffic_algorithmic"] = t.get("algorithmic_bytes_per_launch")
             break
-        result["kernels"] = {
-            L.PROBE_NAMES[kk]: {"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None,
-                                "frac": round(v[0] / (v[1] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4) if v[1] > 0 else None,
-                                "ms_per_step": round(v[1] / 2, 3), "launches_per_step": v[2] // 2}
-            for kk, v in probes.items() if v[2]}
+        # MFMA classes priced in TFLOP/s against the bf16 peak; the HBM-bound slab reduce of a k-split
+        # grouped dW in GB/s against the HBM peak
+        result["kernels"] = {}
+        for kk, v in probes.items():
+            if not v[2]:
+                continue
+            ent = {"ms_per_step": round(v[1] / 2, 3), "launches_per_step": v[2] // 2}
+            if kk == L.PROBE_DW_SLAB:
+                gbs = v[3] / (v[1] * 1e-3) / 1e9 if v[1] > 0 else None
+                ent.update({"gbps": round(gbs, 1) if gbs else None,
+                            "frac_hbm": round(gbs / PEAK_HBM_GBS, 4) if gbs else None})
+            else:
+                ent.update({"tflops": round(v[0] / (v[1] * 1e-3) / 1e12, 1) if v[1] > 0 else None,
+                            "frac": round(v[0] / (v[1] * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4) if v[1] > 0 else None})
+            result["kernels"][L.PROBE_NAMES[kk]] = ent
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, c)
     if rank == 0:

@@ -25,15 +25,17 @@ EPI_ROPE = 1024  # rotate-half RoPE of the q / k head columns after the bias (lo
 # cg_gemm_desc.tile: automatic, or one bf16 kernel forced (tests / A/B runs)
 TILE_AUTO, TILE_VEC, TILE_WIDE, TILE_PERS, TILE_PERS_LW = range(5)
 (PROBE_NONE, PROBE_GEMM_DW, PROBE_GEMM_FWD, PROBE_GEMM_DX, PROBE_ATTN_FWD, PROBE_ATTN_DQ, PROBE_ATTN_DKDV,
- PROBE_GEMM_DW_GROUPED, PROBE_GEMM_PERS) = range(9)
+ PROBE_GEMM_DW_GROUPED, PROBE_GEMM_PERS, PROBE_ATTN_BWD, PROBE_DW_SLAB) = range(11)
 PROBE_NAMES = {PROBE_GEMM_DW: "gemm_bf16_dW", PROBE_GEMM_FWD: "gemm_bf16_fwd", PROBE_GEMM_DX: "gemm_bf16_dX",
                PROBE_ATTN_FWD: "attn_fwd_mfma", PROBE_ATTN_DQ: "attn_bwd_dq_mfma",
                PROBE_ATTN_DKDV: "attn_bwd_dkdv_mfma", PROBE_GEMM_DW_GROUPED: "gemm_dw_grouped",
-               PROBE_GEMM_PERS: "gemm_bf16_pers"}
+               PROBE_GEMM_PERS: "gemm_bf16_pers", PROBE_ATTN_BWD: "attn_bwd_fused_mfma",
+               PROBE_DW_SLAB: "dw_slab_reduce"}
 # rocprofv3 kernel-name prefixes of the probed kernel classes (every instantiation whose name
 # starts with the prefix belongs to the class; bench.py / tools/kstats.py sum them)
 PROBE_KERNELS = {PROBE_GEMM_DW_GROUPED: ("gemm_dw_kernel",), PROBE_ATTN_FWD: ("attn_fwd_mfma",),
                  PROBE_ATTN_DQ: ("attn_bwd_dq_mfma",), PROBE_ATTN_DKDV: ("attn_bwd_dkdv_mfma",),
+                 PROBE_ATTN_BWD: ("attn_bwd_fused_mfma",),
                  # the persistent forward / dX class: the eight-wave kernel and its loader-wave
                  # variant, both launched through cg_gemm's persistent path, probed together
                  PROBE_GEMM_PERS: ("gemm_bf16_pers_kernel", "gemm_bf16_lw_kernel")}

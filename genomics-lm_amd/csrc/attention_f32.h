@@ -618,8 +618,7 @@ static inline int attn_bwd_f32mfma_launch(const float* qkv, long long ld, const 
   do {                                                                                                               \
     hipLaunchKernelGGL((attn_bwd_dq_f32mfma<D, NG>), gq, dim3(256), 0, s, qkv, ld, seg, dy, lddy, y, ldy, lse,    \
                        delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);                           \
-    (void)hipFuncSetAttribute((const void*)attn_bwd_dkdv_f32mfma<D, NG>,                                         \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, fa32::LDS + fa32::QC_BYTES);               \
+    cg_func_lds((const void*)attn_bwd_dkdv_f32mfma<D, NG>, fa32::LDS + fa32::QC_BYTES);                            \
     hipLaunchKernelGGL((attn_bwd_dkdv_f32mfma<D, NG>), gk, dim3(256), fa32::LDS + fa32::QC_BYTES, s, qkv, ld, seg, \
                        dy, lddy, lse, delta, dqkv, lddq, T, H, KV, hd, window, seed, thr, dscale, scale);            \
   } while (0)

@@ -585,7 +585,7 @@ float train_p(const cg_model* m) { return m->training ? m->cfg.dropout : 0.0f; }
 // dW groups run from block L-1 downwards.  Order 1 (default since round 4): the short remainder
 // group (L mod G blocks) comes LAST (C4: groups of 5, 5, 2 from the top), so the buckets whose
 // all-reduce can only start after the final dW launch are the short group's (25 MB instead of
-// 63 MB at C4).  Order 0 (cg_set_dw_order): the remainder first (2, 5, 5), so the first buckets
+// 63 MB at C4).  Order 0 (cg_model_opts.dw_remainder_first): the remainder first (2, 5, 5), so the first buckets
 // are final after 2 blocks instead of 5.  tools/bucket_replay.py priced both on one GPU with the
 // all-reduces modelled as CU-holding side-stream kernels: 5/5/2 8.22 / 8.44 ms against 2/5/5
 // 8.31 / 8.63 ms per C4 step at 600 / 300 GB/s bus bandwidth.

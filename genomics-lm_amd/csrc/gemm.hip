@@ -816,6 +816,10 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
     p.rope_mul = (65536 + p.rope_G - 1) / p.rope_G;
     p.rope_uqk = d->rope_heads * hd / 16;
   }
+  // a forced tile names a bf16 kernel: out of range is a caller error, and an fp32-operand product
+  // (which only the f32-MFMA kernels run) cannot honour it
+  if (d->tile < CG_TILE_AUTO || d->tile > CG_TILE_PERS_LW) return CG_EINVAL;
+  if (d->tile != CG_TILE_AUTO && d->in_dtype != CG_BF16) return CG_EUNSUPPORTED;
   int split = d->split_k > 1 ? d->split_k : 1;
   const int bkt = d->in_dtype == CG_BF16 ? bfg::BKT : 16;
   if (d->K == 0) split = 1;
@@ -879,7 +883,7 @@ extern "C" int cg_gemm(const cg_gemm_desc* d, void* stream) {
       k = d->a_kcontig ? (d->b_kcontig ? gemm_bf16_kernel<true, true> : gemm_bf16_kernel<true, false>)
                        : (d->b_kcontig ? gemm_bf16_kernel<false, true> : gemm_bf16_kernel<false, false>);
     }
-    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
+    cg_func_lds((const void*)k, (int)sh);
     // the persistent tile is one probe class (every forward and dX product of the step, all its
     // epilogue specialisations); the other tiles are classed by operand layout
     const int pk = pers ? CG_PROBE_GEMM_PERS
@@ -952,8 +956,7 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   if (!ntiles) return CG_OK;
   if (P.ksplit > 1) P.kc_steps = cg_cdiv(cg_cdiv(P.K, P.ksplit), bfd::BKT);
   const int grid = std::min(P.ntiles, P.max_wg > 0 ? P.max_wg : cg_pers_cus());
-  (void)hipFuncSetAttribute((const void*)gemm_dw_kernel<BM, NS, BNT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            G::SMEM);
+  cg_func_lds((const void*)gemm_dw_kernel<BM, NS, BNT>, G::SMEM);
   double flops = 0, bytes = 0;
   for (int i = 0; i < P.nprod; ++i) {
     const bfd::Prod& q = P.p[i];
@@ -962,14 +965,21 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   }
   cg_probe_begin(CG_PROBE_GEMM_DW_GROUPED, s);
   hipLaunchKernelGGL((gemm_dw_kernel<BM, NS, BNT>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
-  // the probe window is the grouped kernel alone (the k-split slab reduce is its own kernel in
-  // rocprof's table and is not priced against the MFMA peak)
+  // the probe window is the grouped kernel alone; the k-split slab reduce is its own HBM-bound
+  // probe class (CG_PROBE_DW_SLAB), so a plan that splits the tokens carries its slab pass in the
+  // kernel tables instead of looking cheaper than it is
   cg_probe_end(CG_PROBE_GEMM_DW_GROUPED, s, flops, bytes);
   if (P.ksplit > 1) {
     long long most = 0;
-    for (int i = 0; i < P.nprod; ++i) most = std::max<long long>(most, (long long)P.p[i].N_out * P.p[i].K_out / 4);
+    double elems = 0;
+    for (int i = 0; i < P.nprod; ++i) {
+      most = std::max<long long>(most, (long long)P.p[i].N_out * P.p[i].K_out / 4);
+      elems += (double)P.p[i].N_out * P.p[i].K_out;
+    }
+    cg_probe_begin(CG_PROBE_DW_SLAB, s);
     hipLaunchKernelGGL(dw_slab_reduce_kernel, dim3((unsigned)std::min<long long>(cg_cdiv(most, 256), 512), P.nprod),
                        dim3(256), 0, s, P);
+    cg_probe_end(CG_PROBE_DW_SLAB, s, (P.ksplit - 1) * elems, (4.0 * (P.ksplit - 1) + 8.0) * elems);
   }
   CG_LAUNCH_CHECK();
   return CG_OK;

@@ -938,11 +938,7 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, flo
   if (dtok && V <= EMB_V2 && d % 2 == 0 && ((uintptr_t)g & 7) == 0) {
     const int nch = EMB_RCHUNKS2 > rows ? rows : EMB_RCHUNKS2;
     const size_t sh = (size_t)4 * V * 128 * sizeof(float);
-    static bool attr2 = false;
-    if (!attr2) {
-      (void)hipFuncSetAttribute((const void*)embed_bwd_tok2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr2 = true;
-    }
+    cg_func_lds((const void*)embed_bwd_tok2_kernel, 160 * 1024);
     hipLaunchKernelGGL(embed_bwd_tok2_kernel, dim3(cg_cdiv(d, 128), nch), dim3(256), sh, s, idx, g, (float*)ws, rows,
                        V, d, drop_seed, thr, dscale);
     CG_LAUNCH_CHECK();
@@ -954,11 +950,7 @@ extern "C" int cg_embed_bwd(const int64_t* idx, const float* g, float* dtok, flo
     if (nch > rows) nch = rows;
     const size_t sh = (size_t)4 * V * 64 * sizeof(float);
     if (sh > 160 * 1024) return CG_EUNSUPPORTED;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)embed_bwd_tok_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      attr = true;
-    }
+    cg_func_lds((const void*)embed_bwd_tok_kernel, 160 * 1024);
     hipLaunchKernelGGL(embed_bwd_tok_kernel, dim3(cg_cdiv(d, 64), nch), dim3(256), sh, s, idx, g, (float*)ws, rows,
                        V, d, drop_seed, thr, dscale);
     CG_LAUNCH_CHECK();
@@ -2107,11 +2099,7 @@ __global__ __launch_bounds__(1024) void diag_occupy_kernel(long long ticks) {
 extern "C" int cg_diag_occupy(int n_cus, int usec, void* stream) {
   if (n_cus <= 0 || usec <= 0) return CG_OK;
   if (usec > 10 * 1000 * 1000) return CG_EINVAL;  // bounded: at most 10 s
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)diag_occupy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
+  cg_func_lds((const void*)diag_occupy_kernel, 160 * 1024);
   hipLaunchKernelGGL(diag_occupy_kernel, dim3(n_cus), dim3(1024), 160 * 1024, (hipStream_t)stream,
                      (long long)usec * 100);
   CG_LAUNCH_CHECK();

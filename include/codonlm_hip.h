@@ -536,7 +536,10 @@ enum {
   CG_PROBE_GEMM_DW_GROUPED = 7, /* grouped weight-gradient GEMM (gemm_dw_kernel)     */
   CG_PROBE_GEMM_PERS = 8,      /* persistent fwd / dX GEMM (gemm_bf16_pers_kernel, all */
                                /* epilogue specialisations: one kernel class)           */
-  CG_PROBE_ATTN_BWD = 9        /* attn_bwd_fused_mfma (the fused dQ / dK / dV pass)     */
+  CG_PROBE_ATTN_BWD = 9,       /* attn_bwd_fused_mfma (the fused dQ / dK / dV pass)     */
+  CG_PROBE_DW_SLAB = 10        /* dw_slab_reduce_kernel: the k-split slab sum after the */
+                               /* grouped dW (HBM-bound; work = its adds, bytes = slabs */
+                               /* read + dW read and written)                           */
 };
 int cg_probe_enable(int kind);
 /* record 1 of every `every` launches of the probed kernel (default 1 = all); the launch

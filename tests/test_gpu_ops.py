@@ -737,6 +737,21 @@ def test_gemm_wide_tile(mode, ak, bk, M, N, K):
     assert (outb.float().cpu() - (ref + bias)).abs().max().item() <= tol + 0.05 * (ref + bias).abs().max().item()
 
 
+def test_gemm_forced_tile_errors():
+    """A forced tile is a bf16 kernel: an unknown code is CG_EINVAL and a forced tile on fp32 operands
+    is CG_EUNSUPPORTED (both ValueError), never a silent run of the f32-MFMA kernel."""
+    ops = _ops()
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    a = torch.randn(256, 256, device=DEV)
+    for t in (-1, 5, 7):
+        with pytest.raises(ValueError):
+            ops.gemm(a.to(torch.bfloat16), a.to(torch.bfloat16), tile=t)
+    for t in (L.TILE_VEC, L.TILE_WIDE, L.TILE_PERS, L.TILE_PERS_LW):
+        with pytest.raises(ValueError):
+            ops.gemm(a, a, tile=t)
+    ops.gemm(a, a, tile=L.TILE_AUTO)  # fp32 on the automatic choice still runs
+
+
 def test_transpose16_batch():
     ops = _ops()
     g = torch.Generator().manual_seed(5)
