@@ -138,7 +138,7 @@ def cpu_baseline(cfg_name, c, budget_s=80.0):
         tr.step(x, y, dropout_seed=1000 + len(times))
         times.append(time.perf_counter() - s)
     step = float(np.mean(times))
-    return {"value": Bc * T / step, "unit": "tokens/s", "cores": threads, "kind": "port",
+    return {"value": Bc * T / step, "unit": "tokens/s", "cores": threads, "kind": "port", "batch": Bc,
             "cpu": _cpu_model(), "host_cpus": os.cpu_count(), "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "warmup": nw, "measured": len(times), "ms_per_step": round(step * 1e3, 1),
             "ms_per_step_std": round(float(np.std(times)) * 1e3, 1),
@@ -426,6 +426,10 @@ def main():
             result["kernels"][L.PROBE_NAMES[kk]] = ent
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(args.config, c)
+        # the two sides run different batches (the CPU at the reference's default per-device batch, the
+        # GPU at one optimizer step's sequences as one microbatch): both stated, so the ratio is read
+        # with its batch-size effect in view
+        result["cpu_baseline"]["gpu_batch"] = B
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

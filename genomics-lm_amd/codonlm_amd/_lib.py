@@ -105,7 +105,8 @@ class TransposeBatch(C.Structure):
 class ModelOpts(C.Structure):
     """cg_model_opts: all zero = the measured defaults"""
     _fields_ = [("dw_group", i32), ("dw_ksplit", i32), ("dw_remainder_first", i32), ("head_dw_separate", i32),
-                ("rope_tables", i32), ("attn_mask_kernel", i32), ("dw_plan_tokens", i32), ("attn_bwd_algo", i32)]
+                ("rope_tables", i32), ("attn_mask_kernel", i32), ("dw_plan_tokens", i32), ("attn_bwd_algo", i32),
+                ("pers_max_wg", i32)]
 
 
 class ModelCfg(C.Structure):

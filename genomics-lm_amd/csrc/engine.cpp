@@ -36,7 +36,8 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   if (!c || c->n_embd <= 0 || c->n_head <= 0 || c->n_embd % c->n_head) return false;
   // engine options (zero = defaults): out-of-range values are an error, not a silent default
   if (c->opts.dw_group < 0 || c->opts.dw_ksplit < 0 || c->opts.dw_ksplit > 3 || c->opts.dw_plan_tokens < 0 ||
-      c->opts.attn_bwd_algo < CG_ATTN_BWD_AUTO || c->opts.attn_bwd_algo > CG_ATTN_BWD_FUSED)
+      c->opts.attn_bwd_algo < CG_ATTN_BWD_AUTO || c->opts.attn_bwd_algo > CG_ATTN_BWD_FUSED ||
+      c->opts.pers_max_wg < 0)
     return false;
   D.V = c->vocab_size;
   D.Vp = (int)rup(c->vocab_size, 16);
@@ -462,6 +463,7 @@ cg_gemm_desc gdesc(const Ctx& C) {
   g.c_dtype = C.dt;
   g.alpha = 1.0f;
   g.split_k = 1;
+  g.max_wg = C.m->cfg.opts.pers_max_wg;
   return g;
 }
 
@@ -682,6 +684,7 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
   const int d = D.d;
   cg_dw_group grp;
   memset(&grp, 0, sizeof(grp));
+  grp.max_wg = C.m->cfg.opts.pers_max_wg;
   grp.K = (int)C.M;
   int ks = D.dw_ks;
   grp.tile_m = l_hi - l_lo + 1 == D.G ? D.dw_bm : dw_tile_for(D, l_hi - l_lo + 1, nullptr, &ks, C.M);
@@ -746,6 +749,7 @@ int aux_backward(const Ctx& C, int accumulate) {
   // grouped launch after the loop, as the blocks' dW; their dY operands stay in per-head buffers)
   cg_dw_group grp;
   memset(&grp, 0, sizeof(grp));
+  grp.max_wg = C.m->cfg.opts.pers_max_wg;
   grp.K = (int)M;
   grp.tile_m = 128;  // 10 products of d x d at C5: the 128-row tile gives the most workgroups
   if (m->cfg.termination_aux) {

@@ -252,7 +252,8 @@ int cg_attn_bwd_rope(int dtype, const void* qkv, long long ldqkv, const int32_t*
                      long long ld_part, const float* rope_cos, const float* rope_sin, void* ws,
                      size_t ws_bytes, void* stream);
 /* ABI 0.5: cg_attn_bwd_rope with the bf16 MFMA backward's algorithm chosen per call.
- *   CG_ATTN_BWD_AUTO  (0): the fused pass when B * KV >= the device's CU count, else the split pass
+ *   CG_ATTN_BWD_AUTO  (0): the split pass (measured faster in the step at every benchmarked geometry,
+ *                          profiles/round6/attn_bwd_fused_ab.txt)
  *   CG_ATTN_BWD_SPLIT (1): two kernels -- dQ (S, dP, dQ per query tile), then dK / dV (S, dP, dV,
  *                          dK per key tile): seven MFMA products per tile
  *   CG_ATTN_BWD_FUSED (2): one pass per (batch, kv head) -- S, dP, dV, dK and dQ, five products per
@@ -395,6 +396,9 @@ typedef struct {
   int dw_plan_tokens;     /* > 0: plan the grouped dW as for steps of this many tokens (a small  */
                           /* parity step then runs a large step's plan); 0: the step's own B*T  */
   int attn_bwd_algo;      /* ABI 0.5: CG_ATTN_BWD_* for every block's attention backward (0 auto) */
+  int pers_max_wg;        /* ABI 0.5: grid cap of every persistent launch (grouped dW, persistent */
+                          /* fwd / dX GEMMs); 0 = one workgroup per CU.  A data-parallel run sets */
+                          /* cg_pers_cus() - R to leave R CUs to the bucket all-reduce's kernels  */
 } cg_model_opts;
 typedef struct {
   int vocab_size, block_size, n_layer, n_head, n_kv_head, n_embd;

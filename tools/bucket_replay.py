@@ -15,6 +15,10 @@ group plan -- the planner's own choice, 5/5/2, 4/4/4, 3/3/3/3, 6/6 (remainder gr
 and each (NCH, busbw) pair.  Interleaved rounds, min and median.
 
     BR_B=32 python tools/bucket_replay.py [busbw_GBs ...]     (BR_B: sequences per GPU, default 32)
+
+BR_PLANS=planner limits the plans; BR_RESERVE=8,16 adds the planner's plan with every persistent
+launch capped at cg_pers_cus() - R workgroups (cg_model_opts.pers_max_wg), the CUs a data-parallel
+run would leave to RCCL's kernels.
 """
 import os
 import statistics
@@ -39,6 +43,11 @@ def main():
     busbws = [float(a) for a in sys.argv[1:]] or [300.0, 600.0]
     dev = torch.device("cuda", 0)
     models = {}
+    plans = [p for p in PLANS if p[0] in os.environ.get("BR_PLANS", ",".join(n for n, _ in PLANS)).split(",")]
+    cus = int(L.lib.cg_pers_cus())
+    for r in [int(v) for v in os.environ.get("BR_RESERVE", "").split(",") if v]:
+        plans.append((f"res{r}", {"pers_max_wg": cus - r}))
+    PLANS[:] = plans
     for name, opts in PLANS:  # one model per plan (the plan is part of the model's configuration)
         torch.manual_seed(0)
         m = TinyGPT(68, 1024, n_layer=12, n_head=8, n_embd=512, dropout=0.1, label_smoothing=0.05,
@@ -91,7 +100,7 @@ def main():
             times[(plan, nch, bw)].append(s.elapsed_time(e) / 5)
     for (plan, nch, bw), t in times.items():
         tag = "no comm" if not nch else f"{nch:2d} CUs, busbw {bw:4.0f} GB/s"
-        print(f"plan {plan:6s} {tag:28s} step {min(t):6.3f} ms (median {statistics.median(t):6.3f})", flush=True)
+        print(f"plan {plan:7s} {tag:28s} step {min(t):6.3f} ms (median {statistics.median(t):6.3f})", flush=True)
 
 
 if __name__ == "__main__":
