@@ -67,7 +67,7 @@ DW_MAX = 32
 
 class DwProduct(C.Structure):
     _fields_ = [("A", vp), ("lda", i64), ("B", vp), ("ldb", i64), ("C", vp), ("ldc", i64),
-                ("N_out", i32), ("K_out", i32), ("alpha", f32), ("accumulate", i32)]
+                ("N_out", i32), ("K_out", i32), ("alpha", f32), ("accumulate", i32), ("col_sum", vp)]
 
 
 class DwGroup(C.Structure):

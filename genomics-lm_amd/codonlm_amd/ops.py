@@ -379,9 +379,10 @@ def transpose16(mats):
 
 def gemm_dw_grouped(products, *, tile_m=0, ksplit=1):
     """Grouped weight gradients: for each (dy [K, N_out] bf16, x [K, K_out] bf16, out fp32
-    [N_out, K_out], alpha, accumulate) -> out (+)= alpha * dy^T x, one persistent launch
+    [N_out, K_out], alpha, accumulate[, col_sum]) -> out (+)= alpha * dy^T x, one persistent launch
     (cg_gemm_dw_grouped).  Row strides are taken from the tensors.  ksplit > 1: each tile's K rows
-    split over that many workgroups (fp32 slabs + one in-order reduction)."""
+    split over that many workgroups (fp32 slabs + one in-order reduction).  col_sum (fp32 [N_out],
+    optional): (+)= alpha * the column sums of dy (the bias gradient), ksplit 1 only."""
     if not products:
         return
     if len(products) > L.DW_MAX:
@@ -389,7 +390,7 @@ def gemm_dw_grouped(products, *, tile_m=0, ksplit=1):
     g = L.DwGroup()
     g.n, g.tile_m = len(products), int(tile_m)
     K = None
-    for i, (dy, x, out, alpha, acc) in enumerate(products):
+    for i, (dy, x, out, alpha, acc, *cs) in enumerate(products):
         for t in (dy, x, out):
             L.require_device(t, "gemm_dw_grouped")
         if dy.dtype != torch.bfloat16 or x.dtype != torch.bfloat16 or out.dtype != torch.float32:
@@ -405,6 +406,11 @@ def gemm_dw_grouped(products, *, tile_m=0, ksplit=1):
         if tuple(out.shape) != (p.N_out, p.K_out):
             raise ValueError("gemm_dw_grouped: out must be [N_out, K_out]")
         p.alpha, p.accumulate = float(alpha), int(bool(acc))
+        if cs and cs[0] is not None:
+            L.require_device(cs[0], "gemm_dw_grouped")
+            if cs[0].dtype != torch.float32 or cs[0].numel() != p.N_out or not cs[0].is_contiguous():
+                raise ValueError("gemm_dw_grouped: col_sum must be a contiguous fp32 [N_out]")
+            p.col_sum = cs[0].data_ptr()
     g.K = int(K)
     ws = None
     if ksplit > 1:

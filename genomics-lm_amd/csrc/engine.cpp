@@ -677,6 +677,28 @@ int head_dw_now(const Ctx& C, long long hoff, float alpha, int accumulate) {
 
 namespace {
 
+// The tile code and the token split the grouped dW launch of blocks [l_lo, l_hi] runs with (the
+// split only where the slab workspace exists)
+int group_plan(const Ctx& C, int l_hi, int l_lo, int* ks_out) {
+  const Dims& D = C.D;
+  int ks = D.dw_ks;
+  const int tile = l_hi - l_lo + 1 == D.G ? D.dw_bm : dw_tile_for(D, l_hi - l_lo + 1, nullptr, &ks, C.M);
+  *ks_out = (ks > 1 && C.A.dwslab) ? ks : 1;
+  return tile;
+}
+// fc1's bias gradient (the column sums of dH) comes from block l's grouped dW launch when that
+// launch does not split the tokens (gemm_dw.h CS variant); else from the dGELU product's epilogue
+bool fc1_bias_in_dw(const Ctx& C, int l) {
+  const Dims& D = C.D;
+  if (C.dt != CG_BF16 || D.swiglu) return false;
+  const int top = l + slot_of(D, l);
+  int lo = top;
+  while (!group_ends(D, lo)) --lo;
+  int ks = 1;
+  group_plan(C, top, lo, &ks);
+  return ks == 1;
+}
+
 // The weight gradients of blocks [l_lo, l_hi] from their kept operands: one grouped launch in
 // bf16 mode (gemm_dw.h), the per-product GEMMs in fp32 parity mode.
 int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
@@ -686,9 +708,9 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
   memset(&grp, 0, sizeof(grp));
   grp.max_wg = C.m->cfg.opts.pers_max_wg;
   grp.K = (int)C.M;
-  int ks = D.dw_ks;
-  grp.tile_m = l_hi - l_lo + 1 == D.G ? D.dw_bm : dw_tile_for(D, l_hi - l_lo + 1, nullptr, &ks, C.M);
-  if (ks > 1 && C.A.dwslab) {
+  int ks = 1;
+  grp.tile_m = group_plan(C, l_hi, l_lo, &ks);
+  if (ks > 1) {
     grp.ksplit = ks;
     grp.workspace = C.A.dwslab;
     grp.ws_bytes = C.A.nb.dwslab;
@@ -710,6 +732,7 @@ int flush_dw(const Ctx& C, int l_hi, int l_lo, int accumulate) {
     if (!D.swiglu) {
       CK(add(sl.gin, d, a.g, D.hid, o.w2));
       CK(add(sl.dmlp, D.hid, a.h2, d, o.w1));
+      if (C.dt == CG_BF16 && ks == 1) grp.p[grp.n - 1].col_sum = G(C, o.b1);  // fc1_bias_in_dw
     } else {
       CK(add(sl.gin, d, a.s, D.Hp, o.wd));
       CK(add(sl.dmlp, 2 * D.Hp, a.h2, d, o.wgu));
@@ -1153,13 +1176,19 @@ extern "C" int cg_model_backward(cg_model* m, int phase, int layer, int accumula
     // gradients of the block are produced by its group's flush_dw from the slot operands
     if (!D.swiglu) {
       // (b2's gradient was produced by the LayerNorm backward that wrote gin)
-      // dGELU product; its fused column sums (64-row partials) are fc1's bias gradient
+      // dGELU product.  fc1's bias gradient: the column sums of dH, taken by the block's grouped dW
+      // launch from the dH fragments it streams anyway (round 6; the dGELU epilogue's column sums
+      // cost this product 16-22 us per layer at C4), or -- when that launch splits the tokens --
+      // by this product's fused column-sum epilogue (64-row partials)
+      const bool in_dw = fc1_bias_in_dw(C, l);
       cg_gemm_desc g = lin_dx(C, sl.gin, d, o.w2, D.hid, d, D.hid, sl.dmlp, D.hid, a.w2T);
-      g.epilogue = CG_EPI_DGELU | CG_EPI_GELU_DERIV | CG_EPI_COLSUM; g.aux = a.a; g.ld_aux = D.hid;
-      g.workspace = sl.cpart;
-      g.ws_bytes = A.nb.cpart;
+      g.epilogue = CG_EPI_DGELU | CG_EPI_GELU_DERIV | (in_dw ? 0 : CG_EPI_COLSUM); g.aux = a.a; g.ld_aux = D.hid;
+      if (!in_dw) {
+        g.workspace = sl.cpart;
+        g.ws_bytes = A.nb.cpart;
+      }
       CK(cg_gemm(&g, C.s));
-      CK(defer_reduce(m, sl.cpart, D.hid, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
+      if (!in_dw) CK(defer_reduce(m, sl.cpart, D.hid, (int)((M + 63) / 64), D.hid, G(C, o.b1), accumulate, C.s));
       g = lin_dx(C, sl.dmlp, D.hid, o.w1, d, D.hid, d, A.dsmall, d, a.w1T);  // dL/d(ln2 out), compute dtype
       CK(cg_gemm(&g, C.s));
     } else {

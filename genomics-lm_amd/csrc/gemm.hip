@@ -945,6 +945,9 @@ extern "C" int cg_gemm_dw_tiles(int bm, int N_out, int K_out) {
 template <int BM, int NS, int BNT = bfd::BN>
 static int launch_dw(bfd::Params& P, hipStream_t s) {
   using G = bfd::Geo<BM, NS, BNT>;
+  bool cs = false;
+  for (int i = 0; i < P.nprod; ++i) cs |= P.p[i].colsum != nullptr;
+  auto kern = cs ? gemm_dw_kernel<BM, NS, BNT, true> : gemm_dw_kernel<BM, NS, BNT, false>;
   int ntiles = 0;
   for (int i = 0; i < P.nprod; ++i) {
     bfd::Prod& pr = P.p[i];
@@ -956,7 +959,7 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
   if (!ntiles) return CG_OK;
   if (P.ksplit > 1) P.kc_steps = cg_cdiv(cg_cdiv(P.K, P.ksplit), bfd::BKT);
   const int grid = std::min(P.ntiles, P.max_wg > 0 ? P.max_wg : cg_pers_cus());
-  cg_func_lds((const void*)gemm_dw_kernel<BM, NS, BNT>, G::SMEM);
+  cg_func_lds((const void*)kern, G::SMEM);
   double flops = 0, bytes = 0;
   for (int i = 0; i < P.nprod; ++i) {
     const bfd::Prod& q = P.p[i];
@@ -964,7 +967,7 @@ static int launch_dw(bfd::Params& P, hipStream_t s) {
     bytes += 2.0 * P.K * ((double)q.N_out + q.K_out) + (q.accum ? 8.0 : 4.0) * q.N_out * (double)q.K_out;
   }
   cg_probe_begin(CG_PROBE_GEMM_DW_GROUPED, s);
-  hipLaunchKernelGGL((gemm_dw_kernel<BM, NS, BNT>), dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(G::THREADS), G::SMEM, s, P);
   // the probe window is the grouped kernel alone; the k-split slab reduce is its own HBM-bound
   // probe class (CG_PROBE_DW_SLAB), so a plan that splits the tokens carries its slab pass in the
   // kernel tables instead of looking cheaper than it is
@@ -1015,6 +1018,8 @@ extern "C" int cg_gemm_dw_grouped(const cg_dw_group* grp, void* stream) {
     pr.C = q.C; pr.ldc = q.ldc;
     pr.N_out = q.N_out; pr.K_out = q.K_out;
     pr.alpha = q.alpha; pr.accum = q.accumulate;
+    pr.colsum = q.col_sum;
+    if (q.col_sum && grp->ksplit > 1) return CG_EUNSUPPORTED;
   }
   if (!P.nprod) return CG_OK;
   P.ksplit = grp->ksplit > 1 ? grp->ksplit : 1;

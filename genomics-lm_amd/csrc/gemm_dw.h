@@ -66,6 +66,7 @@ struct Prod {
   int N_out, K_out, tiles_n, tile0;
   float alpha;
   int accum;
+  float* colsum;  // [N_out] (+)= alpha * sum_m A[m][n], or null (kernel CS variant only)
 };
 struct Params {
   Prod p[CG_DW_MAX];
@@ -82,7 +83,12 @@ struct Params {
 };
 }  // namespace bfd
 
-template <int BM, int NSTAGE, int BNT>
+// CS: the launch has a product with a column-sum output (Prod::colsum).  Every wave then also sums
+// the dY fragments it feeds to the MFMAs (v_dot2 against (1, 1): 4 VALU per 8-token fragment, in
+// the MFMAs' shadow); the even waves (wn = 0: every dY column of the tile once) of a product's first
+// column tile write the sums -- the bias gradient for free where a separate pass or a GEMM-epilogue
+// column sum would re-read or hold the whole dY.
+template <int BM, int NSTAGE, int BNT, bool CS>
 __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_dw_kernel(const bfd::Params P) {
   using namespace bfd;
   using G = Geo<BM, NSTAGE, BNT>;
@@ -156,6 +162,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
   };
 
   v4f acc[4][JN];
+  float cs[4];
   auto step = [&](int g) {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * G::DPS) : "memory");
     __builtin_amdgcn_s_barrier();
@@ -222,6 +229,21 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 4 * JN, 0);
     }
+    if constexpr (CS) {
+      // lane l: dY column wm + 16 i + (l & 15), tokens 8 (l >> 4) .. + 7 of each 32-token half
+      typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+      const bf2_t one2 = __builtin_bit_cast(bf2_t, 0x3F803F80u);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint4 u = __builtin_bit_cast(uint4, af[h][i]);
+          cs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.x), one2, cs[i], false);
+          cs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.y), one2, cs[i], false);
+          cs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.z), one2, cs[i], false);
+          cs[i] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf2_t, u.w), one2, cs[i], false);
+        }
+    }
     advance();
   };
 
@@ -234,6 +256,19 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
     const int lt = tile - pr.tile0;
     const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BNT;
     const int g4 = lane >> 4, r16 = lane & 15;
+    if constexpr (CS) {
+      // the four lane groups hold the column's four token subsets (ksplit is 1 with a colsum)
+      if (pr.colsum && n0 == 0 && wn == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = cs[i];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int m = m0 + wm + 16 * i + r16;
+          if (g4 == 0 && m < pr.N_out) pr.colsum[m] = v * pr.alpha + (pr.accum ? pr.colsum[m] : 0.f);
+        }
+      }
+    }
     if (sl > 0) {  // a later token slice: its partial to the slab (dense [N_out][K_out])
       float* slab = P.slab + (long long)(sl - 1) * P.slab_stride + P.slab_off[pi];
 #pragma unroll
@@ -279,6 +314,8 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < JN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cs[i] = 0.f;
     for (int t = 0; t < nt; ++t, ++g) step(g);
     epilogue(k);
   }

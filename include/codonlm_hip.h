@@ -112,6 +112,9 @@ typedef struct {
   float* C; long long ldc;
   int N_out, K_out;
   float alpha; int accumulate;
+  float* col_sum;  /* ABI 0.5, optional: [N_out] fp32 (+)= alpha * sum_m A_p[m][n] (the bias gradient */
+                   /* of the nn.Linear whose output gradient A_p is), from the A fragments the tiles  */
+                   /* already stream; NULL = none; needs ksplit <= 1 (else CG_EUNSUPPORTED)           */
 } cg_dw_product;
 typedef struct {
   int n, K, tile_m;

@@ -54,6 +54,26 @@ def _rel(a, b):
     return float((a - b).norm() / max(float(b.norm()), 1e-30))
 
 
+def _fc1_bias_mask(m):
+    """Flat-gradient mask of the fc1 biases (mlp.0.bias).  Their gradient, the column sums of dH,
+    comes from the block's grouped dW launch (bf16 dH, the fragments the tiles stream) when that
+    launch does not split the tokens, else from the dGELU product's epilogue (fp32 dH before its
+    bf16 rounding): plans with different token splits differ there by dH's rounding, so those
+    entries are compared at 1e-3 and everything else at the plan-invariance bound."""
+    flat = m.flat_parameters()
+    mask = torch.zeros(flat.numel(), dtype=torch.bool, device=flat.device)
+    for k, v in m.named_parameters():
+        if k.endswith("mlp.0.bias"):
+            off = v.data_ptr() // 4 - flat.data_ptr() // 4
+            mask[off:off + v.numel()] = True
+    return mask
+
+
+def _same_grads(g, ref, mask, bound=1e-6):
+    assert _rel(g[~mask], ref[~mask]) < bound, _rel(g[~mask], ref[~mask])
+    assert _rel(g[mask], ref[mask]) < 1e-3, _rel(g[mask], ref[mask])
+
+
 def test_head_dw_defer_on_equals_off():
     on, off = _grads(True, False), _grads(False, False)
     assert on.keys() == off.keys()
@@ -88,14 +108,15 @@ def test_dw_group_orders_give_the_same_gradients():
         _, loss = m(x, y)
         loss.backward()
         torch.cuda.synchronize()
-        return m.flat_grads().detach().clone(), fired
+        return m.flat_grads().detach().clone(), fired, _fc1_bias_mask(m)
 
-    ref, fired_ref = run(0, 1)
+    ref, fired_ref, mask = run(0, 1)
     assert sorted(map(str, fired_ref)) == sorted(map(str, ["head", "embed", *range(12)]))
+    assert int(mask.sum()) == 12 * 512
     for order, group in ((0, 5), (1, 5), (0, 4), (1, 6), (1, 12)):
-        g, fired = run(order, group)
+        g, fired, _ = run(order, group)
         assert sorted(map(str, fired)) == sorted(map(str, fired_ref)), (order, group, fired)
-        assert _rel(g, ref) < 1e-6, (order, group)
+        _same_grads(g, ref, mask)
 
 
 @pytest.mark.parametrize("hd,dropout", [(48, 0.0), (64, 0.1), (32, 0.1)])
@@ -164,9 +185,10 @@ def test_dw_ksplit_gives_the_same_gradients():
     cfg.opts.dw_ksplit = 4  # out of range: an error, not a silent default
     assert L.lib.cg_model_dw_plan(C.byref(cfg), 8, 512, C.byref(G), C.byref(tm), C.byref(ks)) == L.CG_EINVAL
     cfg.opts.dw_ksplit = 0
-    ref = run(1)[0]
+    ref, m1 = run(1)
+    mask = _fc1_bias_mask(m1)
     assert float(ref.abs().max()) > 0
     for ks in (0, 2, 3):
         g = run(ks)[0]
-        assert _rel(g, ref) < 1e-6, (ks, _rel(g, ref))
+        _same_grads(g, ref, mask)
         assert torch.equal(g, run(ks)[0]), ks  # deterministic: slabs reduced in slice order

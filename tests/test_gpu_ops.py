@@ -412,6 +412,40 @@ def test_gemm_dw_grouped_tiles(tile, K, ksplit):
             assert torch.equal(o2, out)
 
 
+@pytest.mark.parametrize("K", [2048, 1023, 37])
+@pytest.mark.parametrize("tile", [128, 129, 256, 512])
+def test_gemm_dw_grouped_colsum(tile, K):
+    """The grouped dW's column-sum output (cg_dw_product.col_sum: the bias gradient of the
+    nn.Linear, the column sums of dY taken from the fragments the tiles stream) for every tile
+    code: products with and without it in one launch, alpha and accumulate, ragged N_out (partial
+    row tiles) and K.  The dW results stay as without it (bitwise), the sums within fp32 summation
+    order of the exact bf16 values (1e-5 of the scale); with a token split it is CG_EUNSUPPORTED."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(7 * tile + K)
+    shapes = [(2048, 512), (200, 136), (512, 384), (72, 520)]
+    prods, plain, refs = [], [], []
+    for i, (n, k) in enumerate(shapes):
+        dy = _bf(torch.randn(K, n, generator=g) + 0.3).to(DEV, torch.bfloat16)
+        x = _bf(torch.randn(K, k, generator=g)).to(DEV, torch.bfloat16)
+        alpha, acc = (0.5, True) if i % 2 else (1.0, False)
+        out = torch.randn(n, k, generator=g).to(DEV)
+        cs = torch.randn(n, generator=g).to(DEV) if i != 2 else None
+        ref = alpha * dy.float().sum(0) + (cs.clone() if acc else 0) if cs is not None else None
+        prods.append((dy, x, out.clone(), alpha, acc, cs))
+        plain.append((dy, x, out.clone(), alpha, acc))
+        refs.append(ref)
+    ops.gemm_dw_grouped(prods, tile_m=tile)
+    ops.gemm_dw_grouped(plain, tile_m=tile)
+    torch.cuda.synchronize()
+    for p, q, ref in zip(prods, plain, refs):
+        assert torch.equal(p[2], q[2])
+        if ref is not None:
+            err = ((p[5] - ref).abs().max() / ref.abs().max()).item()
+            assert err <= 1e-5, (tile, K, tuple(p[2].shape), err)
+    with pytest.raises(ValueError):
+        ops.gemm_dw_grouped(prods[:1], tile_m=tile, ksplit=2)
+
+
 @pytest.mark.parametrize("B,T,H,KV,hd,p", [(2, 1024, 8, 8, 64, 0.1), (2, 200, 4, 2, 48, 0.0), (1, 130, 2, 1, 32, 0.1)])
 def test_attention_bwd_bias_partials(B, T, H, KV, hd, p):
     """The q/k/v bias-gradient partials written by the MFMA attention backward reduce to the

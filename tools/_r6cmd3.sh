@@ -1,0 +1,8 @@
+export TMPDIR=/tmp
+for v in base new; do
+  O=gpurun_out/r6prof_$v; mkdir -p $O
+  if [ $v = base ]; then export CG_LIB_PATH=var/base/libcodonlm_hip.so; else unset CG_LIB_PATH; fi
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O -o run --output-format csv -- python bench.py --no-cpu-baseline --no-kernel-roofline --steps 20 --warmup 5 > $O/bench.log 2>&1 || exit 1
+done
+unset CG_LIB_PATH
+for v in base new; do echo "== $v"; python tools/kstats.py $(ls gpurun_out/r6prof_$v/run_kernel_stats.csv gpurun_out/r6prof_$v/*/run_kernel_stats.csv 2>/dev/null | head -1) 25 12; done
