@@ -152,7 +152,8 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
     }
   };
   auto issue = [&](int g) {
-    const uint32_t st = lds0 + (g % S) * G::STAGE_BYTES + wave * 1024;
+    // (readfirstlane: the M0 operand of the LDS-DMA must stay scalar whatever the optimiser does with g)
+    const uint32_t st = __builtin_amdgcn_readfirstlane(lds0 + (g % S) * G::STAGE_BYTES + wave * 1024);
     const uint32_t ao = a_org + dt * a_step, bo = b_org + dt * b_step;
 #pragma unroll
     for (int i = 0; i < G::A_CHUNKS; ++i) dma16_asm(ra, st + G::WAVES * i * 1024, ao + va[i]);
@@ -163,7 +164,8 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
 
   v4f acc[4][JN];
   float cs[4];
-  auto step = [&](int g) {
+  auto step = [&](int g, auto cs_c) __attribute__((always_inline)) {
+    constexpr bool TCS = decltype(cs_c)::value;  // this tile sums its dY fragments
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 2) * G::DPS) : "memory");
     __builtin_amdgcn_s_barrier();
     const char* st = smem + (g % S) * G::STAGE_BYTES;
@@ -177,7 +179,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
 #pragma unroll
     for (int j = 0; j < JN; ++j) bfr[0][j] = bfg::frag<false>(bs, bc + 16 * j, 0, lane);
     // the DMAs of stage g + S - 1 go into the slot step g - 1 read (every wave is past it)
-    const uint32_t nx = lds0 + ((g + S - 1) % S) * G::STAGE_BYTES + wave * 1024;
+    const uint32_t nx = __builtin_amdgcn_readfirstlane(lds0 + ((g + S - 1) % S) * G::STAGE_BYTES + wave * 1024);
     const uint32_t ao = a_org + dt * a_step, bo = b_org + dt * b_step;
     if constexpr (JN == 4) {
 #pragma unroll
@@ -229,7 +231,7 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
       }
       __builtin_amdgcn_sched_group_barrier(0x008, 4 * JN, 0);
     }
-    if constexpr (CS) {
+    if constexpr (TCS) {
       // lane l: dY column wm + 16 i + (l & 15), tokens 8 (l >> 4) .. + 7 of each 32-token half
       typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
       const bf2_t one2 = __builtin_bit_cast(bf2_t, 0x3F803F80u);
@@ -256,19 +258,6 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
     const int lt = tile - pr.tile0;
     const int m0 = (lt / pr.tiles_n) * BM, n0 = (lt % pr.tiles_n) * BNT;
     const int g4 = lane >> 4, r16 = lane & 15;
-    if constexpr (CS) {
-      // the four lane groups hold the column's four token subsets (ksplit is 1 with a colsum)
-      if (pr.colsum && n0 == 0 && wn == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float v = cs[i];
-          v += __shfl_xor(v, 16);
-          v += __shfl_xor(v, 32);
-          const int m = m0 + wm + 16 * i + r16;
-          if (g4 == 0 && m < pr.N_out) pr.colsum[m] = v * pr.alpha + (pr.accum ? pr.colsum[m] : 0.f);
-        }
-      }
-    }
     if (sl > 0) {  // a later token slice: its partial to the slab (dense [N_out][K_out])
       float* slab = P.slab + (long long)(sl - 1) * P.slab_stride + P.slab_off[pi];
 #pragma unroll
@@ -314,9 +303,37 @@ __global__ __launch_bounds__((bfd::Geo<BM, NSTAGE, BNT>::THREADS), 1) void gemm_
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < JN; ++j) acc[i][j] = (v4f){0.f, 0.f, 0.f, 0.f};
+    // only the first column tile of a product with a column-sum output pays the sums' VALU (the
+    // branch is per tile, outside the k-loop, so the loop bodies keep their MFMA schedule, and the
+    // sums are live only in that branch)
+    int cpi = -1;
+    if constexpr (CS) {
+      const int tile = (lb + k * nblk) / P.ksplit;
+      int pi;
+      find(tile, pi);
+      if (P.p[pi].colsum && (tile - P.p[pi].tile0) % P.p[pi].tiles_n == 0) cpi = pi;
+    }
+    if (cpi >= 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) cs[i] = 0.f;
-    for (int t = 0; t < nt; ++t, ++g) step(g);
+      for (int i = 0; i < 4; ++i) cs[i] = 0.f;
+      for (int t = 0; t < nt; ++t, ++g) step(g, std::true_type{});
+      // the even waves (wn = 0) hold every dY column of the tile once; the four lane groups hold
+      // the column's four token subsets (ksplit is 1 with a column sum)
+      const Prod& pr = P.p[cpi];
+      if (wn == 0) {
+        const int m0 = ((lb + k * nblk) - pr.tile0) / pr.tiles_n * BM;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float v = cs[i];
+          v += __shfl_xor(v, 16);
+          v += __shfl_xor(v, 32);
+          const int m = m0 + wm + 16 * i + (lane & 15);
+          if ((lane >> 4) == 0 && m < pr.N_out) pr.colsum[m] = v * pr.alpha + (pr.accum ? pr.colsum[m] : 0.f);
+        }
+      }
+    } else {
+      for (int t = 0; t < nt; ++t, ++g) step(g, std::false_type{});
+    }
     epilogue(k);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA may land after the workgroup ends
