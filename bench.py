@@ -361,7 +361,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (uniform random codons 4..67, resident in HBM; random-init weights)",
+        "data": "synthetic (uniform random codons 4..67, pre-staged in HBM: the trainer's one per-batch gather "
+                "launch, cg_gather_windows, is not in the timed step; random-init weights)",
         "config": {"workload": f"TinyGPT {c['n_layer']}L{c['n_head']}H d{c['n_embd']} T{T} V68 "
                                + ("eval forward" if fwd_only else "train step")
                                + (" + 5 offset heads + termination head (trainer objective)" if aux and not fwd_only
