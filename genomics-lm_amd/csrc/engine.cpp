@@ -26,6 +26,8 @@ enum { SITE_EMB = 0, SITE_ATTN = 1, SITE_MLP = 2 };
 
 struct Dims {
   int V, Vp, Tmax, L, H, KV, d, hd, kvd, Nqkv, hid, Hp, swiglu, rope;
+  int Vh;  // split-bf16 dlogits half width: Vp rounded to 32, so the head dX product's K = 2 Vh is a
+           // multiple of the persistent tile's 64-deep k-step
   int G, dw_bm, dw_ks;  // blocks per grouped weight-gradient launch, its tile rows, token split
   int force_ks;         // cfg.opts.dw_ksplit: 0 = the planner's choice
   bool rem_first;       // cfg.opts.dw_remainder_first
@@ -41,6 +43,7 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
     return false;
   D.V = c->vocab_size;
   D.Vp = (int)rup(c->vocab_size, 16);
+  D.Vh = (int)rup(D.Vp, 32);
   D.Tmax = c->block_size;
   D.L = c->n_layer;
   D.H = c->n_head;
@@ -257,8 +260,8 @@ struct Acts {
   void* xf;
   // backward scratch
   void *dlogits, *dbig, *dsmall;
-  void* head2;  // bf16 mode: the head weight stacked twice [E; E] (2Vp x d), K operand of the split-dlogits dX
-  long long ldl;  // dlogits row stride: Vp, or 2 Vp for split bf16 (hi | lo)
+  void* head2;  // bf16 mode: [E^T 0 | E^T 0] (d x 2Vh, K-contiguous), B operand of the split-dlogits dX
+  long long ldl;  // dlogits row stride: Vp, or 2 Vh for split bf16 (hi in [0, Vh) | lo in [Vh, 2Vh))
   float *g, *dtmp, *delta, *lnpart, *colws, *splitws, *embws, *cews;
   float* bpart;  // qkv bias-gradient partials from the attention backward [B*ceil(T/128)][Nqkv]
   float* dwslab;  // bf16: the grouped dW's token-split slabs (null when no group splits)
@@ -317,7 +320,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
   A.odpj.assign(noff, nullptr); A.oda.assign(noff, nullptr); A.odl.assign(noff, nullptr);
   A.ocp.assign(noff, nullptr);
   const size_t es_dl = c->dtype == CG_BF16 ? 2 : 4;
-  const long long ldl_ = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
+  const long long ldl_ = c->dtype == CG_BF16 ? 2LL * D.Vh : D.Vp;
   char* opj_all = noff ? w.take<char>((size_t)noff * M * d * es) : nullptr;
   char* odl_all = noff ? w.take<char>((size_t)noff * M * ldl_ * es_dl) : nullptr;
   A.nb.ocp_half = cg_colsum_workspace((int)M, d);
@@ -330,7 +333,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
     A.oa[i] = w.take<char>(M * d * es);
     A.og[i] = w.take<char>(M * d * es);
   }
-  A.ldl = c->dtype == CG_BF16 ? 2LL * D.Vp : D.Vp;
+  A.ldl = ldl_;
   A.dlogits = w.take<char>(M * A.ldl * es);
   A.slot.resize(D.G);
   A.nb.lnp = cg_layernorm_bwd_workspace((int)M, d, 1);
@@ -345,7 +348,7 @@ size_t carve(const cg_model_cfg* c, const Dims& D, int B, int T, char* base, Act
     sl.cpart = w.take<float>(A.nb.cpart);
     sl.bpart = w.take<float>((size_t)B * ((T + 127) / 128) * D.Nqkv * 4);
   }
-  A.head2 = c->dtype == CG_BF16 ? w.take<char>((size_t)2 * D.Vp * d * 2) : nullptr;
+  A.head2 = c->dtype == CG_BF16 ? w.take<char>((size_t)2 * D.Vh * d * 2) : nullptr;
   const long long big = std::max<long long>({(long long)D.hid, 2LL * D.Hp, (long long)D.Nqkv});
   A.dbig = w.take<char>(M * big * es);
   A.dsmall = w.take<char>(M * std::max(d, D.Hp) * es);
@@ -492,26 +495,31 @@ cg_gemm_desc lin_dx(const Ctx& C, const void* dy, long long lddy, long long woff
   return g;
 }
 // d[M,d] (fp32, + resid epilogue set by the caller) = dl[M,Vp] . E[Vp,d] for a head weight E:
-// in bf16 mode dl holds split-bf16 rows (hi | lo, CG_BF16X2) and the product runs over
-// K = 2 Vp against [E; E] (A.head2, filled by fill_head2)
+// in bf16 mode dl holds split-bf16 rows (hi | lo, CG_BF16X2, halves Vh wide with zero pads) and the
+// product runs over K = 2 Vh against [E^T 0 | E^T 0] (A.head2, filled by fill_head2): both operands
+// K-contiguous and K a multiple of 64, so it runs on the persistent tile (round 6; it was the
+// register-staged vector kernel with an MN-contiguous [E; E], 27.6 us at C4)
 cg_gemm_desc head_dx(const Ctx& C, long long hoff, void* out, long long ldo, const void* dl = nullptr) {
   const Dims& D = C.D;
   if (!dl) dl = C.A.dlogits;
   if (C.dt != CG_BF16) return lin_dx(C, dl, D.Vp, hoff, D.d, D.Vp, D.d, out, ldo);
   cg_gemm_desc g = gdesc(C);
-  g.M = (int)C.M; g.N = D.d; g.K = 2 * D.Vp;
+  g.M = (int)C.M; g.N = D.d; g.K = 2 * D.Vh;
   g.A = dl; g.lda = C.A.ldl; g.a_kcontig = 1;
-  g.B = C.A.head2; g.ldb = D.d; g.b_kcontig = 0;
+  g.B = C.A.head2; g.ldb = 2 * D.Vh; g.b_kcontig = 1;
   g.C = out; g.ldc = ldo;
   return g;
 }
 int fill_head2(const Ctx& C, long long hoff) {
   if (C.dt != CG_BF16) return CG_OK;
-  const size_t bytes = (size_t)C.D.Vp * C.D.d * 2;
+  const Dims& D = C.D;
+  // zero pad columns [Vp, Vh) of each half (the matching dlogits pads are zero too), then E^T twice
+  if (hipMemsetAsync(C.A.head2, 0, (size_t)2 * D.Vh * D.d * 2, C.s) != hipSuccess) return CG_ELAUNCH;
+  cg_transpose_batch tb;
+  tb.n = 2;
   for (int i = 0; i < 2; ++i)
-    if (hipMemcpyAsync((char*)C.A.head2 + i * bytes, W(C, hoff), bytes, hipMemcpyDeviceToDevice, C.s) != hipSuccess)
-      return CG_ELAUNCH;
-  return CG_OK;
+    tb.items[i] = cg_transpose_item{W(C, hoff), (char*)C.A.head2 + (size_t)i * D.Vh * 2, D.d, 2LL * D.Vh, D.Vp, D.d};
+  return cg_transpose16_batch(&tb, C.s);
 }
 // refresh the transposed weight copies of every block (one batched launch per 64 matrices)
 int transpose_weights(const Ctx& C) {
@@ -838,7 +846,8 @@ int aux_backward(const Ctx& C, int accumulate) {
       continue;
     }
     if (!m->aux_ready) return CG_EINVAL;
-    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.odl[i], A.ldl, D.Vp, C.s));
+    CK(cg_cast_pad_2d(dl, D.V, (int)M, D.V, C.dt == CG_BF16 ? CG_BF16X2 : C.dt, A.odl[i], A.ldl,
+                      C.dt == CG_BF16 ? D.Vh : D.Vp, C.s));
     // dpj = Gc . E ; the second Linear's grads
     void* dpj = A.odpj[i];
     void* da = A.oda[i];
