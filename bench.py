@@ -170,6 +170,8 @@ def main():
     ap.add_argument("--no-kernel-roofline", action="store_true")
     ap.add_argument("--attn-bwd", default="auto", choices=["auto", "split", "fused"],
                     help="bf16 attention backward (cg_model_opts.attn_bwd_algo; A/B runs, default automatic)")
+    ap.add_argument("--engine-opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="a cg_model_opts field for A/B runs (repeatable; all zero = the measured defaults)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -184,6 +186,10 @@ def main():
     from codonlm_amd.optim import FusedAdamW
     from codonlm_amd.training.ddp import DataParallelStep
 
+    engine_opts = {"attn_bwd_algo": {"auto": 0, "split": 1, "fused": 2}[args.attn_bwd]}
+    for kv in args.engine_opt:
+        k, v = kv.split("=", 1)
+        engine_opts[k] = int(v)
     c = dict(CONFIGS[args.config])
     B = args.batch or c["batch"]
     T = c["block_size"]
@@ -193,7 +199,7 @@ def main():
                     label_smoothing=0.05, n_kv_head=c["kv"], use_swiglu=c["swiglu"], use_rope=c["rope"],
                     termination_aux=bool(c.get("term")), multi_offset_targets=list(c.get("offsets", ())) or None,
                     compute_dtype=args.dtype, device=dev,
-                    engine_opts={"attn_bwd_algo": {"auto": 0, "split": 1, "fused": 2}[args.attn_bwd]})
+                    engine_opts=engine_opts)
     if world > 1:  # identical replicas
         dist.broadcast(model.flat_parameters(), 0)
     model.train()
@@ -371,7 +377,9 @@ def main():
                    "micro_batch_per_gpu": B, "parallelism": f"dp{world}", "dropout": 0.1,
                    "label_smoothing": 0.05, "sep_mask": True,
                    "path": args.path if (not aux or fwd_only) else "trainer",
-                   **({"attn_bwd": args.attn_bwd} if args.attn_bwd != "auto" else {})},
+                   **({"attn_bwd": args.attn_bwd} if args.attn_bwd != "auto" else {}),
+                   **({"engine_opts": {k: v for k, v in engine_opts.items() if v}}
+                      if any(v for v in engine_opts.values()) else {})},
         "final_loss": round(final_loss, 4),
         "model_flops_per_token": ftok,
         "step_mfma_frac": round(value / world * ftok / (PEAK_BF16_TFLOPS * 1e12), 4),

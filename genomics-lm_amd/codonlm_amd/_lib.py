@@ -144,6 +144,8 @@ SIGNATURES = {
     "cg_gemm_dw_grouped": (i32, [C.POINTER(DwGroup), vp]),
     "cg_gemm_dw_tiles": (i32, [i32, i32, i32]),
     "cg_layernorm_fwd": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, vp]),
+    "cg_layernorm_fwd_mask": (i32, [i32, vp, i64, vp, vp, vp, i64, vp, vp, i32, i32, f32, i32, i32, i32, u32, f32, vp,
+                                    vp]),
     "cg_layernorm_bwd_blocks": (i32, [i32]),
     "cg_layernorm_bwd_workspace": (sz, [i32, i32, i32]),
     "cg_layernorm_bwd": (i32, [i32, vp, i64, vp, i64, vp, vp, vp, vp, vp, i32, vp, u32, f32, vp, sz, vp, vp,

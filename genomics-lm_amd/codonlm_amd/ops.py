@@ -98,6 +98,23 @@ def layernorm_fwd(x, weight, bias, out_dtype=torch.float32, eps=1e-5):
     return y, mean, rstd
 
 
+def layernorm_fwd_mask(x, weight, bias, B, T, H, drop_seed, drop_p, out_dtype=torch.bfloat16, eps=1e-5):
+    """cg_layernorm_fwd_mask: layernorm_fwd and the attention-dropout keep words (attn_drop_mask) in one
+    launch -> (y, mean, rstd, mask)."""
+    L.require_device(x, "layernorm_fwd_mask")
+    rows, cols = x.shape
+    y = torch.empty(rows, cols, dtype=out_dtype, device=x.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty_like(mean)
+    n = int(L.lib.cg_attn_drop_mask_bytes(B, T, H))
+    mask = torch.zeros(max(n, 4) // 4, dtype=torch.int32, device=x.device)
+    L.check(L.lib.cg_layernorm_fwd_mask(_dt(y), x.data_ptr(), x.stride(0), weight.data_ptr(), bias.data_ptr(),
+                                        y.data_ptr(), y.stride(0), mean.data_ptr(), rstd.data_ptr(), rows, cols, eps,
+                                        B, T, H, int(drop_seed) & 0xFFFFFFFF, float(drop_p), mask.data_ptr(),
+                                        L.stream_ptr(x.device)), "cg_layernorm_fwd_mask")
+    return y, mean, rstd, mask
+
+
 def layernorm_bwd(dy, x, mean, rstd, weight, g_in=None, eps=1e-5, branch_dtype=None, drop_seed=0, drop_p=0.0):
     """LayerNorm backward.  With `branch_dtype`, also returns the consumer-branch copy of g_out
     (dropout-masked with (drop_seed, drop_p)) and its column sums (the producing Linear's bias grad):

@@ -379,45 +379,12 @@ __device__ __forceinline__ int lo_of(const int32_t* seg, long long rowbase, int 
 // blocks above the diagonal are never written and never consumed (those pairs are causally
 // masked before the bit test).
 // ============================================================================
-// acc = 2 acc + (half SEL of h >= thr): v_cmp (SDWA word select) into VCC, v_addc shifts it in
-template <int SEL>
-__device__ __forceinline__ uint32_t shift_in_keep(uint32_t acc, uint32_t h, uint32_t thr) {
-  uint32_t r;
-  if constexpr (SEL == 0)
-    asm("v_cmp_ge_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc"
-        : "=v"(r) : "v"(h), "s"(thr), "v"(acc) : "vcc");
-  else
-    asm("v_cmp_ge_u32_sdwa vcc, %1, %2 src0_sel:WORD_1 src1_sel:DWORD\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc"
-        : "=v"(r) : "v"(h), "s"(thr), "v"(acc) : "vcc");
-  return r;
-}
-
 __global__ __launch_bounds__(256) void attn_drop_mask_kernel(uint32_t* __restrict__ qmask, int T, int wpr,
                                                              uint32_t seed, uint32_t thr, int nbt) {
   // 4 waves per workgroup, one 64x64 block each (one-wave workgroups were dispatch-bound)
   const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (i >= nbt) return;
-  int qb = (int)((sqrtf(8.f * (float)i + 1.f) - 1.f) * 0.5f);
-  while ((qb + 1) * (qb + 2) / 2 <= i) ++qb;
-  while (qb * (qb + 1) / 2 > i) --qb;
-  const int kb = i - qb * (qb + 1) / 2;
-  const long long bh = blockIdx.y;
-  const int q = qb * 64 + (int)(threadIdx.x & 63);
-  if (q >= T) return;
-  const uint32_t hrow = cg_row_hash(seed, (uint32_t)(bh * T + q));
-  uint32_t wq[2];
-#pragma unroll
-  for (int w = 0; w < 2; ++w) {
-    uint32_t ev = 0, od = 0;
-#pragma unroll
-    for (int c = 15; c >= 0; --c) {  // high pairs first: pair c lands on bits c / 16 + c
-      const uint32_t h = cg_pair_mix(hrow + (uint32_t)(kb * 32 + w * 16 + c) * CG_COLK);
-      ev = shift_in_keep<0>(ev, h, thr);
-      od = shift_in_keep<1>(od, h, thr);
-    }
-    wq[w] = ev | (od << 16);
-  }
-  *(uint2*)(qmask + ((bh * (wpr >> 1) + kb) * T + q) * 2) = make_uint2(wq[0], wq[1]);
+  cg_drop_mask_block(qmask, T, wpr, seed, thr, i, (long long)blockIdx.y, (int)(threadIdx.x & 63));
 }
 
 // ============================================================================

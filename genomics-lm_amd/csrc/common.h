@@ -89,6 +89,47 @@ __device__ __forceinline__ bool cg_keep(uint32_t seed, uint32_t row, uint32_t co
   uint32_t bits = (col & 1u) ? (h >> 16) : (h & 0xFFFFu);
   return bits >= thr;
 }
+// ---- the attention-dropout keep words of one 64x64 block of the causal lower triangle (query
+// block qb, key block kb of triangle index i) for row bh = b*H + h: keep = cg_keep(seed,
+// bh*T + q, key, thr), one wave, lane = query; per key pair one hash, two compares, two shift-ins
+// (10 VALU ops).  Words in "pair-split" order (bit c = key 2c, bit 16 + c = key 2c + 1) at
+// qmask[((bh*(wpr/2) + kb)*T + q)*2 + w] (attention_mfma.h attn_drop_mask_kernel, and beside the
+// LayerNorm rows in ops.hip ln_fwd_mask_kernel).
+// acc = 2 acc + (half SEL of h >= thr): v_cmp (SDWA word select) into VCC, v_addc shifts it in
+template <int SEL>
+__device__ __forceinline__ uint32_t cg_shift_in_keep(uint32_t acc, uint32_t h, uint32_t thr) {
+  uint32_t r;
+  if constexpr (SEL == 0)
+    asm("v_cmp_ge_u32_sdwa vcc, %1, %2 src0_sel:WORD_0 src1_sel:DWORD\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc"
+        : "=v"(r) : "v"(h), "s"(thr), "v"(acc) : "vcc");
+  else
+    asm("v_cmp_ge_u32_sdwa vcc, %1, %2 src0_sel:WORD_1 src1_sel:DWORD\n\tv_addc_co_u32_e32 %0, vcc, %3, %3, vcc"
+        : "=v"(r) : "v"(h), "s"(thr), "v"(acc) : "vcc");
+  return r;
+}
+__device__ __forceinline__ void cg_drop_mask_block(uint32_t* __restrict__ qmask, int T, int wpr, uint32_t seed,
+                                                   uint32_t thr, int i, long long bh, int lane) {
+  int qb = (int)((sqrtf(8.f * (float)i + 1.f) - 1.f) * 0.5f);
+  while ((qb + 1) * (qb + 2) / 2 <= i) ++qb;
+  while (qb * (qb + 1) / 2 > i) --qb;
+  const int kb = i - qb * (qb + 1) / 2;
+  const int q = qb * 64 + lane;
+  if (q >= T) return;
+  const uint32_t hrow = cg_row_hash(seed, (uint32_t)(bh * T + q));
+  uint32_t wq[2];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    uint32_t ev = 0, od = 0;
+#pragma unroll
+    for (int c = 15; c >= 0; --c) {  // high pairs first: pair c lands on bits c / 16 + c
+      const uint32_t h = cg_pair_mix(hrow + (uint32_t)(kb * 32 + w * 16 + c) * CG_COLK);
+      ev = cg_shift_in_keep<0>(ev, h, thr);
+      od = cg_shift_in_keep<1>(od, h, thr);
+    }
+    wq[w] = ev | (od << 16);
+  }
+  *(uint2*)(qmask + ((bh * (wpr >> 1) + kb) * T + q) * 2) = make_uint2(wq[0], wq[1]);
+}
 __host__ __device__ inline uint32_t cg_drop_threshold(float p) {
   float t = p * 65536.0f + 0.5f;
   uint32_t u = (uint32_t)t;

@@ -39,7 +39,7 @@ bool dims_of(const cg_model_cfg* c, Dims& D) {
   // engine options (zero = defaults): out-of-range values are an error, not a silent default
   if (c->opts.dw_group < 0 || c->opts.dw_ksplit < 0 || c->opts.dw_ksplit > 3 || c->opts.dw_plan_tokens < 0 ||
       c->opts.attn_bwd_algo < CG_ATTN_BWD_AUTO || c->opts.attn_bwd_algo > CG_ATTN_BWD_FUSED ||
-      c->opts.pers_max_wg < 0)
+      c->opts.pers_max_wg < 0 || c->opts.attn_mask_kernel < 0 || c->opts.attn_mask_kernel > 2)
     return false;
   D.V = c->vocab_size;
   D.Vp = (int)rup(c->vocab_size, 16);
@@ -970,6 +970,9 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
   // mask kernel right before it (cfg.opts.attn_mask_kernel; a mask pass on a side stream ahead of
   // the forward measured slower, round 2)
   const bool fused_keep = !m->cfg.opts.attn_mask_kernel;
+  // attn_mask_kernel 2: the keep words made in the launch of the block's LN1 (cg_layernorm_fwd_mask),
+  // read by the forward (round 6)
+  const bool mask_in_ln = m->cfg.opts.attn_mask_kernel == 2;
   const bool rope_epi = !m->cfg.opts.rope_tables;
   CK(cg_segment_starts(idx, A.seg, B, T, m->cfg.sep_id, C.s));
   CK(cg_embed_fwd(idx, P(C, C.Lo.tok), C.Lo.pos >= 0 ? P(C, C.Lo.pos) : nullptr, A.x, B, T, d,
@@ -979,7 +982,12 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
     const auto& a = A.la[l];
     float* xl = A.x + (size_t)l * M * d;
     float* xn = A.x + (size_t)(l + 1) * M * d;
-    CK(cg_layernorm_fwd(C.dt, xl, d, P(C, o.ln1w), P(C, o.ln1b), a.h1, d, a.mean1, a.rstd1, (int)M, d, eps, C.s));
+    const void* dmask = p > 0.f ? a.dmask : nullptr;
+    if (dmask && mask_in_ln)  // this block's attention keep words beside its LN1 rows (one launch)
+      CK(cg_layernorm_fwd_mask(C.dt, xl, d, P(C, o.ln1w), P(C, o.ln1b), a.h1, d, a.mean1, a.rstd1, (int)M, d, eps, B, T,
+                               D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+    else
+      CK(cg_layernorm_fwd(C.dt, xl, d, P(C, o.ln1w), P(C, o.ln1b), a.h1, d, a.mean1, a.rstd1, (int)M, d, eps, C.s));
     cg_gemm_desc g = lin_fwd(C, a.h1, d, o.wqkv, d, D.Nqkv, d, a.qkv, D.Nqkv);
     g.epilogue = CG_EPI_BIAS; g.bias = P(C, o.bqkv);
     // RoPE in the projection's epilogue where the GEMM tile implements it, else a table pass
@@ -996,12 +1004,11 @@ extern "C" int cg_model_forward(cg_model* m, const int64_t* idx, const int64_t* 
       CK(cg_gemm(&g, C.s));
       if (D.rope) CK(cg_rope_tab(C.dt, a.qkv, D.Nqkv, B, T, D.H, D.KV, D.hd, m->rope_cos, m->rope_sin, 0, C.s));
     }
-    const void* dmask = p > 0.f ? a.dmask : nullptr;
     if (dmask && fused_keep) {
       CK(cg_attn_fwd_keep(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV,
                           D.hd, window, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
     } else {
-      if (dmask) CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
+      if (dmask && !mask_in_ln) CK(cg_attn_drop_mask(B, T, D.H, site_seed(seed, l, SITE_ATTN), p, a.dmask, C.s));
       CK(cg_attn_fwd(C.dt, a.qkv, D.Nqkv, m->cfg.sep_id >= 0 ? A.seg : nullptr, a.y, d, a.lse, B, T, D.H, D.KV, D.hd,
                      window, site_seed(seed, l, SITE_ATTN), p, dmask, C.s));
     }

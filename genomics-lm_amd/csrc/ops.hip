@@ -171,15 +171,13 @@ __global__ __launch_bounds__(256) void ln_fwd_pf(const float* __restrict__ x, lo
   }
 }
 
+// one LayerNorm row per wave (ln_fwd_vec; ln_fwd_mask_kernel)
 template <typename TO, int W, int NV>
-__global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, long long ldx,
-                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                  TO* __restrict__ y, long long ldy, float* __restrict__ mean,
-                                                  float* __restrict__ rstd, int rows, float eps) {
+__device__ __forceinline__ void ln_fwd_row(const float* __restrict__ x, long long ldx, const float* __restrict__ gamma,
+                                           const float* __restrict__ beta, TO* __restrict__ y, long long ldy,
+                                           float* __restrict__ mean, float* __restrict__ rstd, int row, float eps,
+                                           int lane) {
   constexpr int cols = 64 * W * NV;
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
   const float* xr = x + (long long)row * ldx;
   float v[NV][W];
   float s = 0.f;
@@ -213,6 +211,48 @@ __global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, l
   if (lane == 0) {
     if (mean) mean[row] = mu;
     if (rstd) rstd[row] = rs;
+  }
+}
+
+template <typename TO, int W, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_vec(const float* __restrict__ x, long long ldx,
+                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                  TO* __restrict__ y, long long ldy, float* __restrict__ mean,
+                                                  float* __restrict__ rstd, int rows, float eps) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  ln_fwd_row<TO, W, NV>(x, ldx, gamma, beta, y, ldy, mean, rstd, row, eps, threadIdx.x & 63);
+}
+
+// The LayerNorm rows of a block's input (HBM-bound) and the attention-dropout keep words of the same
+// block's attention (VALU-bound: cg_drop_mask_block) in one launch: LayerNorm and keep-word
+// workgroups alternate in the grid, so every CU runs both kinds side by side and the keep words
+// ride on the LayerNorm's memory time.  nln LayerNorm workgroups (4 rows each), nmask keep-word
+// workgroups (4 causal 64x64 blocks each, mbx per (b, h) row).
+template <typename TO, int W, int NV>
+__global__ __launch_bounds__(256) void ln_fwd_mask_kernel(const float* __restrict__ x, long long ldx,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, TO* __restrict__ y,
+                                                          long long ldy, float* __restrict__ mean,
+                                                          float* __restrict__ rstd, int rows, float eps, int nln,
+                                                          uint32_t* __restrict__ qmask, int T, int wpr, uint32_t seed,
+                                                          uint32_t thr, int nbt, int mbx, int nmask) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pair = min(nln, nmask);
+  int role, k;
+  if (b < 2 * pair) {
+    role = b & 1;
+    k = b >> 1;
+  } else {
+    role = nln > nmask ? 0 : 1;
+    k = pair + (b - 2 * pair);
+  }
+  if (role == 0) {
+    const int row = k * 4 + wave;
+    if (row < rows) ln_fwd_row<TO, W, NV>(x, ldx, gamma, beta, y, ldy, mean, rstd, row, eps, lane);
+  } else {
+    const int i = (k % mbx) * 4 + wave;
+    if (i < nbt) cg_drop_mask_block(qmask, T, wpr, seed, thr, i, (long long)(k / mbx), lane);
   }
 }
 
@@ -272,6 +312,54 @@ extern "C" int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, co
                        (float*)y, ldy, mean, rstd, rows, cols, eps);
   CG_LAUNCH_CHECK();
   return CG_OK;
+}
+
+template <typename TO>
+static bool ln_fwd_mask_fast(int W, int cols, hipStream_t s, const float* x, long long ldx, const float* gamma,
+                             const float* beta, TO* y, long long ldy, float* mean, float* rstd, int rows, float eps,
+                             uint32_t* qmask, int B, int T, int H, uint32_t seed, uint32_t thr) {
+  const int nb = cg_cdiv(T, 64), nbt = nb * (nb + 1) / 2, mbx = cg_cdiv(nbt, 4);
+  const long long nmask = (long long)mbx * B * H, nln = cg_cdiv(rows, 4);
+  if (nmask + nln > 0x7fffffffLL) return false;
+  const dim3 g((unsigned)(nmask + nln));
+#define LNFM(WW, N)                                                                                                 \
+  case N:                                                                                                          \
+    hipLaunchKernelGGL((ln_fwd_mask_kernel<TO, WW, N>), g, dim3(256), 0, s, x, ldx, gamma, beta, y, ldy, mean, rstd, \
+                       rows, eps, (int)nln, qmask, T, 2 * nb, seed, thr, nbt, mbx, (int)nmask);                       \
+    return true;
+  if (W == 4) {
+    switch (cols / 256) { LNFM(4, 1) LNFM(4, 2) LNFM(4, 3) LNFM(4, 4) default: return false; }
+  }
+  if (W == 2) {
+    switch (cols / 128) { LNFM(2, 1) LNFM(2, 2) LNFM(2, 3) LNFM(2, 4) LNFM(2, 6) LNFM(2, 8) default: return false; }
+  }
+  return false;
+#undef LNFM
+}
+
+extern "C" int cg_layernorm_fwd_mask(int out_dtype, const float* x, long long ldx, const float* gamma,
+                                     const float* beta, void* y, long long ldy, float* mean, float* rstd, int rows,
+                                     int cols, float eps, int B, int T, int H, uint32_t drop_seed, float drop_p,
+                                     void* mask, void* stream) {
+  if (!(drop_p > 0.f) || drop_p >= 1.f || !mask || B < 0 || T < 0 || H <= 0) return CG_EINVAL;
+  if (cols <= 0 || cols > 64 * LN_MAXV || rows < 0) return CG_EUNSUPPORTED;
+  const uint32_t thr = cg_drop_threshold(drop_p);
+  const int W = ln_width(cols, x, ldx, y, ldy, out_dtype == CG_BF16 ? 2 : 4);
+  if (W && rows > 0 && B > 0 && T > 0) {
+    const bool ok = out_dtype == CG_BF16
+                        ? ln_fwd_mask_fast<bf16_t>(W, cols, (hipStream_t)stream, x, ldx, gamma, beta, (bf16_t*)y, ldy,
+                                                   mean, rstd, rows, eps, (uint32_t*)mask, B, T, H, drop_seed, thr)
+                        : ln_fwd_mask_fast<float>(W, cols, (hipStream_t)stream, x, ldx, gamma, beta, (float*)y, ldy,
+                                                  mean, rstd, rows, eps, (uint32_t*)mask, B, T, H, drop_seed, thr);
+    if (ok) {
+      CG_LAUNCH_CHECK();
+      return CG_OK;
+    }
+  }
+  // shapes outside the vector LayerNorm: the two launches (the same results)
+  const int rc = cg_layernorm_fwd(out_dtype, x, ldx, gamma, beta, y, ldy, mean, rstd, rows, cols, eps, stream);
+  if (rc != CG_OK) return rc;
+  return cg_attn_drop_mask(B, T, H, drop_seed, drop_p, mask, stream);
 }
 
 extern "C" int cg_layernorm_bwd_blocks(int rows) {

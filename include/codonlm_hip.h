@@ -136,6 +136,14 @@ int cg_gemm_dw_tiles(int tile_m, int N_out, int K_out);
 int cg_layernorm_fwd(int out_dtype, const float* x, long long ldx, const float* gamma,
                      const float* beta, void* y, long long ldy, float* mean, float* rstd,
                      int rows, int cols, float eps, void* stream);
+/* ABI 0.5: cg_layernorm_fwd and cg_attn_drop_mask(B, T, H, drop_seed, drop_p, mask) in one launch
+ * (the LayerNorm of a block's input is HBM-bound, the keep words of the same block's attention
+ * dropout VALU-bound: their workgroups alternate in one grid and run side by side).  Results are
+ * those of the two calls, bit for bit; drop_p in (0, 1) and mask non-NULL (else CG_EINVAL). */
+int cg_layernorm_fwd_mask(int out_dtype, const float* x, long long ldx, const float* gamma,
+                          const float* beta, void* y, long long ldy, float* mean, float* rstd,
+                          int rows, int cols, float eps, int B, int T, int H, uint32_t drop_seed,
+                          float drop_p, void* mask, void* stream);
 /* dx = LN backward(dy) [+ g_in]; writes g_out (fp32) and optionally g_out_t (out_dtype,
  * optionally multiplied by a dropout keep mask (seed,p) for the consumer branch);
  * per-block column partials for dgamma/dbeta go to `partials` [nblk][2*cols]
@@ -395,7 +403,8 @@ typedef struct {
   int rope_tables;        /* 1: RoPE as separate cg_rope_tab passes (0: fused into the qkv      */
                           /* projection's epilogue and the attention backward)                  */
   int attn_mask_kernel;   /* 1: the attention dropout keep bits by cg_attn_drop_mask before     */
-                          /* each block's forward (0: written by the attention forward itself)  */
+                          /* each block's forward (0: written by the attention forward itself); */
+                          /* 2 (ABI 0.5): made in the block's LN1 launch, cg_layernorm_fwd_mask */
   int dw_plan_tokens;     /* > 0: plan the grouped dW as for steps of this many tokens (a small  */
                           /* parity step then runs a large step's plan); 0: the step's own B*T  */
   int attn_bwd_algo;      /* ABI 0.5: CG_ATTN_BWD_* for every block's attention backward (0 auto) */

@@ -192,3 +192,30 @@ def test_dw_ksplit_gives_the_same_gradients():
         g = run(ks)[0]
         _same_grads(g, ref, mask)
         assert torch.equal(g, run(ks)[0]), ks  # deterministic: slabs reduced in slice order
+
+
+def test_attention_keep_word_sources_give_the_same_step():
+    """The attention-dropout keep words of a training step made by the attention forward itself
+    (default), by the separate mask kernel (engine option attn_mask_kernel=1) or in the launch of the
+    block's LN1 (attn_mask_kernel=2, cg_layernorm_fwd_mask): the same words, so the same loss and
+    the same gradients, bit for bit (model_tiny_gpt.py:104-114 dropout on the attention
+    probabilities, one mask per step and block)."""
+    from codonlm_amd import TinyGPT
+    x, y = _batch(B=4, T=256, seed=21)
+
+    def run(mode):
+        torch.manual_seed(17)
+        m = TinyGPT(68, 256, n_layer=3, n_head=4, n_embd=256, dropout=0.1, label_smoothing=0.05,
+                    compute_dtype="bf16", device=DEV, engine_opts={"attn_mask_kernel": mode})
+        m.train()
+        m.flat_grads().zero_()
+        _, loss = m(x, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        return float(loss), m.flat_grads().detach().clone()
+
+    l0, g0 = run(0)
+    for mode in (1, 2):
+        lm, gm = run(mode)
+        assert lm == l0, (mode, lm, l0)
+        assert torch.equal(gm, g0), mode

@@ -122,6 +122,44 @@ def test_layernorm_fwd_bwd(out_dtype, cols):
     assert (csum.cpu() - exp_t.sum(0)).abs().max() < 2e-3
 
 
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,cols,B,T,H", [(2048, 512, 2, 1024, 8), (1536, 384, 3, 512, 8), (300, 100, 2, 150, 4),
+                                             (64, 256, 1, 64, 2), (4000, 512, 1, 700, 1)])
+def test_layernorm_fwd_mask_equals_two_launches(out_dtype, rows, cols, B, T, H):
+    """cg_layernorm_fwd_mask (a block's LN1 rows and its attention keep words in one launch, engine
+    option attn_mask_kernel=2) against cg_layernorm_fwd + cg_attn_drop_mask: every output bit for
+    bit, the grid's LayerNorm and keep-word workgroups in every proportion (more rows than mask
+    blocks and the reverse), a LayerNorm width without the vector path (100: the two-launch route),
+    and every causal keep bit against the oracle's dropout_keep."""
+    ops = _ops()
+    g = torch.Generator().manual_seed(rows + cols)
+    x = (torch.randn(rows, cols, generator=g) * 2 + 0.5).to(DEV)
+    w = (1 + 0.1 * torch.randn(cols, generator=g)).to(DEV)
+    b = (0.1 * torch.randn(cols, generator=g)).to(DEV)
+    seed, p = 4242 + T, 0.1
+    y, mean, rstd, mask = ops.layernorm_fwd_mask(x, w, b, B, T, H, seed, p, out_dtype=out_dtype)
+    y2, mean2, rstd2 = ops.layernorm_fwd(x, w, b, out_dtype=out_dtype)
+    ref = torch.zeros_like(mask)
+    import ctypes as C
+    L = __import__("codonlm_amd._lib", fromlist=["x"])
+    L.check(L.lib.cg_attn_drop_mask(B, T, H, seed, C.c_float(p), ref.data_ptr(), L.stream_ptr(x.device)), "mask")
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2) and torch.equal(mean, mean2) and torch.equal(rstd, rstd2)
+    assert torch.equal(mask, ref)
+    # the words decode to the oracle's keep bits on the causal triangle (pair-split order, tile-major)
+    nt = (T + 63) // 64
+    words = mask.cpu().numpy().view(np.uint32)[: B * H * nt * T * 2].reshape(B * H, nt, T, 2)
+    bh = np.arange(B * H)[:, None, None]
+    q = np.arange(T)[None, :, None]
+    k = np.arange(T)[None, None, :]
+    keep = O.dropout_keep(seed, bh * T + q, np.broadcast_to(k, (1, 1, T)), p)
+    kt, kw, kc = k // 64, (k % 64) // 32, k % 32
+    bit = np.where(kc % 2 == 0, kc // 2, 16 + kc // 2)
+    got = (words[bh, kt, q, kw] >> bit) & 1
+    causal = np.broadcast_to(k <= q, got.shape)
+    assert np.array_equal(got[causal].astype(bool), np.broadcast_to(keep, got.shape)[causal])
+
+
 @pytest.mark.parametrize("cols", [512, 100])
 def test_layernorm_bwd_partials_deferred_reduce(cols):
     """The engine's deferred path (row pass writing partials + one batched cg_reduce_columns over
