@@ -219,3 +219,30 @@ def test_attention_keep_word_sources_give_the_same_step():
         lm, gm = run(mode)
         assert lm == l0, (mode, lm, l0)
         assert torch.equal(gm, g0), mode
+
+
+def test_persistent_grid_cap_gives_the_same_step():
+    """cg_model_opts.pers_max_wg (the grid cap a data-parallel run could use to leave CUs to RCCL,
+    priced in profiles/round6/dp_reserve_replay.txt) only changes which workgroup walks which tile:
+    every tile is reduced in the same order, so the loss and every gradient are bitwise those of
+    the uncapped grid (forward / dX persistent GEMMs and the grouped dW launches)."""
+    from codonlm_amd import TinyGPT, _lib as L
+    x, y = _batch(B=4, T=256, seed=23)
+    cus = int(L.lib.cg_pers_cus())
+
+    def run(cap):
+        torch.manual_seed(19)
+        m = TinyGPT(68, 256, n_layer=3, n_head=4, n_embd=256, dropout=0.1, label_smoothing=0.05,
+                    compute_dtype="bf16", device=DEV, engine_opts={"pers_max_wg": cap})
+        m.train()
+        m.flat_grads().zero_()
+        _, loss = m(x, y)
+        loss.backward()
+        torch.cuda.synchronize()
+        return float(loss), m.flat_grads().detach().clone()
+
+    l0, g0 = run(0)
+    for cap in (cus - 16, 37):
+        lc, gc = run(cap)
+        assert lc == l0, (cap, lc, l0)
+        assert torch.equal(gc, g0), cap
