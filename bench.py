@@ -412,6 +412,8 @@ def main():
             t = json.loads(tr.read_text())
             if t.get("probe") != name or t.get("micro_batch", 16) != B:  # (files before round 5: B=16)
                 continue
+            if args.path != "engine":  # the passes ran the engine's training step (tools/prof_round3.sh)
+                continue
             result["roofline"]["traffic"] = t["hbm_bytes_per_launch"]
             result["roofline"]["traffic_unit"] = "HBM bytes/launch (PMC)"
             result["roofline"]["traffic_source"] = (f"{tr.relative_to(ROOT)} "
